@@ -1,0 +1,315 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident GF(2^16) Reed-Solomon encode+decode on MI355X.
+
+Metric (BASELINE.json): "encode+decode GiB/s (device-resident, 1024B shards);
+% of HBM roofline".  A step = one encode (reed_solomon_16::encode,
+src/lib.rs:242-279) plus one decode at 100 % original loss (recovery shards
+0..k given, no originals; benches/benchmarks.rs:82-106) of one stripe of
+32768:32768 x 1024 B shards (BASELINE configs[3], the largest single-GPU
+configuration), inputs resident in HBM, through the C ABI
+(rs16_encode_device / rs16_decode_device).  GiB/s counts
+(original + recovery) bytes for the encode and again for the decode
+(README.md:114-116; benches/benchmarks.rs:56-58).
+
+Multi-GPU (--gpus N, one process per GPU via torch.distributed.run): every
+rank encodes+decodes its own independent stripe (seed = rank), no data-path
+collective; value = all ranks' bytes / max-over-ranks time ("weak").
+
+Also reported: roofline of the dominant kernel (hipEvent-timed live in a
+profiled copy of the timed loop; PMC traffic from profiles/ if present) and
+the CPU baseline (the oracle's C restatement of the reference NoSimd engine,
+1 core, rank 0 at N=1 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import platform
+import socket
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "reed-solomon-16_amd"))
+
+METRIC = "encode+decode GiB/s (device-resident, 1024B shards); % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = 2.0 ** 30
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--original", type=int, default=32768)
+    p.add_argument("--recovery", type=int, default=32768)
+    p.add_argument("--shard-bytes", type=int, default=1024)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extra", action="store_true", help="skip the 1000:1000 side measurements")
+    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def pass_bytes(prog: str, k: int, m: int, S: int) -> float:
+    """Algorithmic HBM bytes of one launch of a pass program (rows read + rows
+    written, S bytes each) for a single-chunk high-rate k:m codec."""
+    chunk = 1 << (m - 1).bit_length()
+    n_dec = 1 << (chunk + k - 1).bit_length()
+    L_enc, L_dec = chunk.bit_length() - 1, n_dec.bit_length() - 1
+    lo_e, lo_d = L_enc // 2, L_dec // 2
+    if prog == "ENC_FIRST":
+        rows = k + chunk
+    elif prog == "ENC_MID":
+        rows = 2 * chunk
+    elif prog == "ENC_LAST":
+        tiles_rows = -(-m // (1 << lo_e)) << lo_e
+        rows = tiles_rows + m
+    elif prog == "DEC_FIRST":
+        rows = k + n_dec  # 100 % loss: k recovery rows read
+    elif prog == "DEC_MID":
+        rows = 2 * n_dec
+    elif prog == "DEC_LAST":
+        t = -(-k // (1 << lo_d)) << lo_d
+        rows = 2 * t + k
+    elif prog == "ENC_SINGLE":
+        rows = k + m
+    elif prog == "DEC_SINGLE":
+        rows = 2 * k
+    else:
+        return 0.0
+    return float(rows) * S
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cpu_baseline(original, recovery, k, m, S, budget_s):
+    """The oracle NoSimd (C restatement of src/engine/engine_nosimd.rs + rates),
+    1 thread, run like the reference bench: per iteration add_original_shard x k
+    + encode, then add_recovery_shard x k + decode (benches/benchmarks.rs:71-106)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_bind as O
+
+    enc = O.Encoder("default", "nosimd", k, m, S)
+    dec = O.Decoder("default", "nosimd", k, m, S)
+    loss = min(k, m)
+    t_total, iters = 0.0, 0
+    while iters == 0 or t_total < budget_s:
+        t0 = time.perf_counter()
+        for s in original:
+            enc.add_original_shard(s)
+        enc.encode()
+        for i in range(k - loss):
+            dec.add_original_shard(i, original[i])
+        for i in range(loss):
+            dec.add_recovery_shard(i, recovery[i])
+        dec.decode()
+        t_total += time.perf_counter() - t0
+        iters += 1
+    gib = 2 * (k + m) * S * iters / GIB
+    return {"value": gib / t_total, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{iters} x (encode + 100%-loss decode) of {k}:{m} x {S} B, {t_total:.1f} s on 1 thread "
+                      f"of {cpu_model()} (nproc {os.cpu_count()}); oracle = C restatement of the reference "
+                      f"NoSimd engine (Rust reference not buildable here)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "LOCAL_RANK" not in os.environ:
+        # Relaunch one process per GPU before anything touches the GPU.
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve())]
+        cmd += sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (barrier, max of times)
+        dist.init_process_group("gloo", init_method="env://")
+
+    import numpy as np
+
+    import rs16
+    from rs16.device import DeviceArray
+    from rs16.util import generate_original
+
+    k, m, S = args.original, args.recovery, args.shard_bytes
+    eng = rs16.Engine(local)
+    seed = rank & 0xFF
+    original = generate_original(k, S, seed)
+    d_orig = DeviceArray.from_numpy(eng, original)
+    d_rec = DeviceArray(eng, m * S)
+    d_rest = DeviceArray(eng, k * S)
+    loss = min(k, m)
+    of = np.ones(k, np.uint8)
+    of[:loss] = 0
+    rf = np.zeros(m, np.uint8)
+    rf[:loss] = 1
+    d_of, d_rf = DeviceArray.from_numpy(eng, of), DeviceArray.from_numpy(eng, rf)
+    if loss < k:
+        d_rest.upload(original)  # received originals stay in place
+
+    def encode():
+        rs16.encode_device(k, m, S, d_orig.ptr, d_rec.ptr, engine=eng)
+
+    def decode():
+        rs16.decode_device(k, m, S, d_rest.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, k - loss, loss, engine=eng)
+
+    # ---- correctness gate (the measured path must be the bit-exact one) ----
+    encode()
+    recovery = d_rec.download(shape=(m, S))
+    verified = "decode restores every original bit-exactly"
+    if seed == 0 and S == 1024:
+        fx = json.loads((ROOT / "tests" / "golden" / "kib_hashes.json").read_text())
+        want = {(c["k"], c["m"]): c["recovery_sha256"] for c in fx["cases"]}.get((k, m))
+        if want is not None:
+            got = hashlib.sha256(recovery.tobytes()).hexdigest()
+            assert got == want, f"recovery hash {got} != oracle fixture {want}"
+            verified = "recovery SHA-256 == oracle fixture; " + verified
+    decode()
+    assert np.array_equal(d_rest.download(shape=(k, S)), original), "decode did not restore the originals"
+
+    def barrier():
+        eng.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    def timed(fn, steps):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        eng.synchronize()
+        dt = time.perf_counter() - t0
+        barrier()
+        if dist is not None:
+            import torch
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+    def step():
+        encode()
+        decode()
+
+    for _ in range(args.warmup):
+        step()
+    dt = timed(step, args.steps)
+    step_bytes = 2 * (k + m) * S  # encode + decode, (original + recovery) bytes each
+    value = world * step_bytes * args.steps / dt / GIB
+    ms_per_step = dt / args.steps * 1e3
+
+    # Separate encode-only / decode-only rates (same data, same engine).
+    dt_e = timed(encode, args.steps)
+    dt_d = timed(decode, args.steps)
+
+    # ---- roofline: dominant kernel, hipEvent-timed on the engine stream ----
+    eng.profile_reset()
+    eng.set_profiling(True)
+    timed(step, args.steps)
+    eng.set_profiling(False)
+    prof = eng.profile()
+    kernels = {name: {"avg_us": ms / n * 1e3, "launches": n} for name, (ms, n) in prof.items()}
+    dom = max(prof, key=lambda p: prof[p][0])
+    dom_avg_s = prof[dom][0] / prof[dom][1] / 1e3
+    alg = pass_bytes(dom, k, m, S)
+    achieved = alg / dom_avg_s / 1e9
+    traffic = None
+    tp = Path(args.traffic_json)
+    if tp.exists():
+        try:
+            tj = json.loads(tp.read_text())
+            key = f"{dom}:{k}:{m}:{S}"
+            traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
+                "algorithmic_bytes_per_launch": alg,
+                "whole_step_frac": round(step_bytes / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    extra = {}
+    if not args.no_extra and (k, m) != (1000, 1000):
+        # BASELINE configs[1] / [2]: 1000:1000 x 1 KiB encode, decode at 100 % loss
+        k2 = m2 = 1000
+        o2 = generate_original(k2, S, seed)
+        a = DeviceArray.from_numpy(eng, o2)
+        r = DeviceArray(eng, m2 * S)
+        x = DeviceArray(eng, k2 * S)
+        f0 = DeviceArray.from_numpy(eng, np.zeros(k2, np.uint8))
+        f1 = DeviceArray.from_numpy(eng, np.ones(m2, np.uint8))
+        e2 = lambda: rs16.encode_device(k2, m2, S, a.ptr, r.ptr, engine=eng)
+        d2 = lambda: rs16.decode_device(k2, m2, S, x.ptr, f0.ptr, r.ptr, f1.ptr, 0, m2, engine=eng)
+        e2()
+        d2()
+        assert np.array_equal(x.download(shape=(k2, S)), o2)
+        for _ in range(args.warmup):
+            e2(); d2()
+        n2 = max(args.steps, 50)
+        te = timed(e2, n2)
+        td = timed(d2, n2)
+        extra["1000:1000x1024"] = {"encode_gib_s": world * (k2 + m2) * S * n2 / te / GIB,
+                                   "decode_gib_s": world * (k2 + m2) * S * n2 / td / GIB,
+                                   "encode_us": te / n2 * 1e6, "decode_us": td / n2 * 1e6}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(original, recovery, k, m, S, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic (ChaCha8 seed=rank stream of the reference benches; inputs resident in HBM)",
+            "config": {"workload": f"{k}:{m} x {S} B encode + 100%-loss decode per GPU (BASELINE configs[3])",
+                       "original_count": k, "recovery_count": m, "shard_bytes": S,
+                       "parallelism": f"independent stripes x {world} (weak, no collective)"},
+            "encode_gib_s": round(world * (k + m) * S * args.steps / dt_e / GIB, 3),
+            "decode_gib_s": round(world * (k + m) * S * args.steps / dt_d / GIB, 3),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels_us": {n: round(v["avg_us"], 2) for n, v in kernels.items()},
+            "extra": extra,
+            "verified": verified,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+/*
+ * rs16.h -- C ABI of the MI355X-native GF(2^16) Reed-Solomon codec.
+ *
+ * This is the drop-in boundary for the hot path of malaire/reed-solomon-16
+ * v0.1.0 (a Rust crate).  Each entry point names the reference interface it
+ * replaces (file:line in the reference tree).  A Rust `impl Engine` /
+ * FFI stub binding these symbols is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every fallible call returns 0 (RS16_OK) or an error code and, if `err`
+ *    is non-NULL, fills it with the code and the payload fields of the
+ *    reference's `Error` variant (src/lib.rs:31-125) in declaration order.
+ *  - Shard arrays are the reference's flat layout (ShardsRefMut,
+ *    src/engine/shards.rs:60-66): shard i starts at byte i*shard_bytes;
+ *    every 64-byte block holds 32 low bytes then 32 high bytes
+ *    (src/algorithm.md:6-32).
+ *  - `_device` / `d_` pointers are HIP device pointers on the engine's
+ *    device; `stream` is a hipStream_t (NULL = the engine's own stream).
+ *    Device-pointer calls are asynchronous on that stream.
+ *  - One engine must not be used from two threads at once (it owns scratch
+ *    workspace); create one engine per device/thread.
+ */
+#ifndef RS16_H
+#define RS16_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- Error -- reed_solomon_16::Error, src/lib.rs:31-125 ---------------- */
+typedef enum rs16_error_code {
+    RS16_OK = 0,
+    RS16_DIFFERENT_SHARD_SIZE = 1,           /* v0 shard_bytes, v1 got */
+    RS16_DUPLICATE_ORIGINAL_SHARD_INDEX = 2, /* v0 index */
+    RS16_DUPLICATE_RECOVERY_SHARD_INDEX = 3, /* v0 index */
+    RS16_INVALID_ORIGINAL_SHARD_INDEX = 4,   /* v0 original_count, v1 index */
+    RS16_INVALID_RECOVERY_SHARD_INDEX = 5,   /* v0 recovery_count, v1 index */
+    RS16_INVALID_SHARD_SIZE = 6,             /* v0 shard_bytes */
+    RS16_NOT_ENOUGH_SHARDS = 7,              /* v0 original_count, v1 original_received_count,
+                                                v2 recovery_received_count */
+    RS16_TOO_FEW_ORIGINAL_SHARDS = 8,        /* v0 original_count, v1 original_received_count */
+    RS16_TOO_MANY_ORIGINAL_SHARDS = 9,       /* v0 original_count */
+    RS16_UNSUPPORTED_SHARD_COUNT = 10,       /* v0 original_count, v1 recovery_count */
+    /* Not in the reference (it has no device and panics on misuse): */
+    RS16_DEVICE_ERROR = 100,                 /* HIP runtime failure, v0 = hipError_t */
+    RS16_INVALID_ARGUMENT = 101              /* engine-op misuse the reference would panic on */
+} rs16_error_code;
+
+typedef struct rs16_error {
+    int32_t code;
+    uint64_t v0, v1, v2;
+} rs16_error;
+
+/* `impl Display for Error` (src/lib.rs:130-222): writes the exact message,
+ * returns its length (excluding NUL); truncates to len-1 bytes. */
+size_t rs16_error_message(const rs16_error* err, char* buf, size_t len);
+
+/* ---- Engine -- trait Engine (src/engine.rs:140-260) ---------------------
+ * rs16_engine_new plays NoSimd::new (src/engine/engine_nosimd.rs:27-35):
+ * it builds the GF tables (src/engine/tables.rs) once per process and
+ * uploads them to the device's HBM. */
+typedef struct rs16_engine rs16_engine;
+rs16_engine* rs16_engine_new(int device, rs16_error* err);
+void rs16_engine_free(rs16_engine* eng);
+int rs16_engine_device(const rs16_engine* eng);
+void* rs16_engine_stream(const rs16_engine* eng);     /* hipStream_t owned by the engine */
+int rs16_engine_synchronize(rs16_engine* eng, void* stream, rs16_error* err);
+
+/* Engine::fft (src/engine.rs:158-165): in-place DIT FFT on shards
+ * [pos, pos+size) of `data` (shard_count x shard_bytes, device).  Outputs
+ * [pos, pos+truncated_size) are exact for any input.  */
+int rs16_engine_fft(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, size_t pos, size_t size,
+                    size_t truncated_size, size_t skew_delta, void* stream, rs16_error* err);
+/* Engine::fft_skew_end (src/engine.rs:222-230): skew_delta = pos + size. */
+int rs16_engine_fft_skew_end(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, size_t pos,
+                             size_t size, size_t truncated_size, void* stream, rs16_error* err);
+/* Engine::ifft (src/engine.rs:188-195).  As in the reference contract,
+ * shards [pos+truncated_size, pos+size) must be zero on input. */
+int rs16_engine_ifft(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, size_t pos, size_t size,
+                     size_t truncated_size, size_t skew_delta, void* stream, rs16_error* err);
+/* Engine::ifft_skew_end (src/engine.rs:242-250). */
+int rs16_engine_ifft_skew_end(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, size_t pos,
+                              size_t size, size_t truncated_size, void* stream, rs16_error* err);
+/* Engine::fwht (src/engine.rs:175) on a device u16[65536]; data beyond
+ * truncated_size must be zero (the only way eval_poly uses it). */
+int rs16_engine_fwht(rs16_engine* eng, uint16_t* d_data, size_t truncated_size, void* stream, rs16_error* err);
+/* Engine::eval_poly (src/engine.rs:207-218) on a device u16[65536]. */
+int rs16_engine_eval_poly(rs16_engine* eng, uint16_t* d_erasures, size_t truncated_size, void* stream,
+                          rs16_error* err);
+/* Engine::mul (src/engine.rs:198): x[] *= log_m, bytes % 64 == 0. */
+int rs16_engine_mul(rs16_engine* eng, void* d_x, size_t bytes, uint16_t log_m, void* stream, rs16_error* err);
+/* Engine::xor (src/engine.rs:201): x[] ^= y[], bytes % 64 == 0. */
+int rs16_engine_xor(rs16_engine* eng, void* d_x, const void* d_y, size_t bytes, void* stream, rs16_error* err);
+/* Engine::xor_within (src/engine.rs:256-259), ranges must not overlap. */
+int rs16_engine_xor_within(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, size_t x, size_t y,
+                           size_t count, void* stream, rs16_error* err);
+/* Engine::formal_derivative (src/engine.rs:233-238); shard_count must be a
+ * power of two (the reference panics on slice bounds otherwise). */
+int rs16_engine_formal_derivative(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, void* stream,
+                                  rs16_error* err);
+
+/* ---- Rates -- src/rate.rs:51-107, src/rate/rate_default.rs:15-64 --------- */
+typedef enum rs16_rate { RS16_RATE_DEFAULT = 0, RS16_RATE_HIGH = 1, RS16_RATE_LOW = 2 } rs16_rate;
+/* Rate::supports / ReedSolomonEncoder::supports (src/reed_solomon.rs:76-84). */
+int rs16_supports(int rate, size_t original_count, size_t recovery_count);
+/* Rate::validate (src/rate.rs:91-106). */
+int rs16_validate(int rate, size_t original_count, size_t recovery_count, size_t shard_bytes, rs16_error* err);
+/* use_high_rate (src/rate/rate_default.rs:15-64): 1 high, 0 low, -1 error. */
+int rs16_use_high_rate(size_t original_count, size_t recovery_count, rs16_error* err);
+/* {High,Low}Rate{Encoder,Decoder}::work_count (rate_high.rs:131-137,301-305; rate_low.rs:131-137,301-305). */
+size_t rs16_encoder_work_count(int high, size_t original_count, size_t recovery_count);
+size_t rs16_decoder_work_count(int high, size_t original_count, size_t recovery_count);
+
+/* ---- Encoder -- RateEncoder (src/rate.rs:113-173) with the Rate chosen
+ *      by `rate`; RS16_RATE_DEFAULT == ReedSolomonEncoder (src/reed_solomon.rs:13-85).
+ *      Work space lives in HBM (EncoderWork, src/rate/encoder_work.rs). */
+typedef struct rs16_encoder rs16_encoder;
+rs16_encoder* rs16_encoder_new(rs16_engine* eng, int rate, size_t original_count, size_t recovery_count,
+                               size_t shard_bytes, rs16_error* err);
+void rs16_encoder_free(rs16_encoder* enc);
+int rs16_encoder_reset(rs16_encoder* enc, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                       rs16_error* err);
+/* add_original_shard (src/rate/encoder_work.rs:49-69); shard in host memory. */
+int rs16_encoder_add_original_shard(rs16_encoder* enc, const void* shard, size_t len, rs16_error* err);
+/* same, shard in device memory (copied on the engine stream). */
+int rs16_encoder_add_original_shard_device(rs16_encoder* enc, const void* d_shard, size_t len, rs16_error* err);
+/* encode (rate_high.rs:44-83 / rate_low.rs:44-83); on success the
+ * EncoderResult (src/encoder_result.rs) is valid until rs16_encoder_result_drop. */
+int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err);
+/* EncoderResult::recovery (src/encoder_result.rs:16-19): device pointer, NULL if index >= recovery_count. */
+const void* rs16_encoder_recovery_device(rs16_encoder* enc, size_t index);
+/* Copy recovery shard `index` to host memory; returns 1 if it exists, 0 if not, <0 on error. */
+int rs16_encoder_recovery_copy(rs16_encoder* enc, size_t index, void* dst, size_t len, rs16_error* err);
+/* Drop for EncoderResult (src/encoder_result.rs:48-52). */
+void rs16_encoder_result_drop(rs16_encoder* enc);
+int rs16_encoder_is_high_rate(const rs16_encoder* enc);
+
+/* ---- Decoder -- RateDecoder (src/rate.rs:179-250); RS16_RATE_DEFAULT ==
+ *      ReedSolomonDecoder (src/reed_solomon.rs:93-183). */
+typedef struct rs16_decoder rs16_decoder;
+rs16_decoder* rs16_decoder_new(rs16_engine* eng, int rate, size_t original_count, size_t recovery_count,
+                               size_t shard_bytes, rs16_error* err);
+void rs16_decoder_free(rs16_decoder* dec);
+int rs16_decoder_reset(rs16_decoder* dec, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                       rs16_error* err);
+/* add_original_shard / add_recovery_shard (src/rate/decoder_work.rs:62-116). */
+int rs16_decoder_add_original_shard(rs16_decoder* dec, size_t index, const void* shard, size_t len, rs16_error* err);
+int rs16_decoder_add_recovery_shard(rs16_decoder* dec, size_t index, const void* shard, size_t len, rs16_error* err);
+int rs16_decoder_add_original_shard_device(rs16_decoder* dec, size_t index, const void* d_shard, size_t len,
+                                           rs16_error* err);
+int rs16_decoder_add_recovery_shard_device(rs16_decoder* dec, size_t index, const void* d_shard, size_t len,
+                                           rs16_error* err);
+/* decode (rate_high.rs:168-247 / rate_low.rs:168-247); DecoderResult valid until drop. */
+int rs16_decoder_decode(rs16_decoder* dec, rs16_error* err);
+/* DecoderResult::restored_original (src/decoder_result.rs:16-19): device pointer or NULL. */
+const void* rs16_decoder_restored_original_device(rs16_decoder* dec, size_t index);
+/* Copy restored original `index` to host; returns 1 if restored, 0 if None, <0 on error. */
+int rs16_decoder_restored_original_copy(rs16_decoder* dec, size_t index, void* dst, size_t len, rs16_error* err);
+/* Drop for DecoderResult (src/decoder_result.rs:44-48). */
+void rs16_decoder_result_drop(rs16_decoder* dec);
+int rs16_decoder_is_high_rate(const rs16_decoder* dec);
+
+/* ---- Device-resident one-shot codec (the benchmark path) -----------------
+ * reed_solomon_16::encode (src/lib.rs:242-279) with originals and recovery
+ * already in HBM: d_original = original_count shards, d_recovery receives
+ * recovery_count shards.  Default rate selection as ReedSolomonEncoder. */
+int rs16_encode_device(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                       const void* d_original, void* d_recovery, void* stream, rs16_error* err);
+/* reed_solomon_16::decode (src/lib.rs:287-344), device-resident: d_original
+ * holds original_count shard slots (received ones valid, flagged by the
+ * device byte array d_original_received); d_recovery holds recovery_count
+ * slots flagged by d_recovery_received.  The host passes the number of
+ * received shards of each kind (for the reference's NotEnoughShards /
+ * nothing-to-do checks).  Lost originals are restored in place into
+ * d_original.  Default rate selection as ReedSolomonDecoder. */
+int rs16_decode_device(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                       void* d_original, const uint8_t* d_original_received, const void* d_recovery,
+                       const uint8_t* d_recovery_received, size_t original_received_count,
+                       size_t recovery_received_count, void* stream, rs16_error* err);
+
+/* ---- Device memory helpers (so FFI callers need no HIP headers) ------- */
+void* rs16_device_alloc(rs16_engine* eng, size_t bytes, rs16_error* err);
+void rs16_device_free(rs16_engine* eng, void* d_ptr);
+int rs16_memcpy_htod(rs16_engine* eng, void* d_dst, const void* src, size_t bytes, void* stream, rs16_error* err);
+int rs16_memcpy_dtoh(rs16_engine* eng, void* dst, const void* d_src, size_t bytes, void* stream, rs16_error* err);
+int rs16_memset_device(rs16_engine* eng, void* d_dst, int value, size_t bytes, void* stream, rs16_error* err);
+
+/* Diagnostics: per-kernel timing.  When enabled, every HBM pass (and the
+ * eval_poly kernel group) is bracketed by hipEvents on its launch stream.
+ * rs16_engine_profile_read synchronizes and returns, for pass program
+ * `prog` (0 .. rs16_prog_count()-1; the last id is eval_poly), the summed
+ * milliseconds and the number of launches since the last reset. */
+int rs16_engine_set_profiling(rs16_engine* eng, int enable, rs16_error* err);
+int rs16_engine_profile_read(rs16_engine* eng, int prog, double* total_ms, uint64_t* launches, rs16_error* err);
+void rs16_engine_profile_reset(rs16_engine* eng);
+int rs16_prog_count(void);
+const char* rs16_prog_name(int prog);
+
+/* Diagnostics: host-side evaluation of the device multiply (same v_perm
+ * byte-table format and code path as the kernels, with v_perm emulated):
+ * out[] = in[] * log_m for `bytes` (multiple of 64) bytes of shard data, with
+ * Engine::mul semantics (log_m 65535 == x1).  Lets CPU-only tests check the
+ * table format against the reference multiply (NoSimd::mul). */
+void rs16_host_mul(const void* in, void* out, size_t bytes, uint16_t log_m);
+
+/* Library/build identification, e.g. "rs16-mi355x gfx950". */
+const char* rs16_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RS16_H */

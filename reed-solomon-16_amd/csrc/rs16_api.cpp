@@ -1,0 +1,606 @@
+// rs16_api.cpp -- C ABI (include/rs16.h): errors, rate selection, the
+// encoder/decoder state machines (EncoderWork / DecoderWork semantics of
+// src/rate/{encoder,decoder}_work.rs) with HBM-resident work space, and the
+// device-resident one-shot codec.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "rs16_engine.hpp"
+
+using namespace rs16;
+
+// ---------------------------------------------------------------------------
+// Errors -- Display of src/lib.rs:130-222.
+// ---------------------------------------------------------------------------
+extern "C" size_t rs16_error_message(const rs16_error* e, char* buf, size_t len) {
+    char tmp[256];
+    unsigned long long a = e->v0, b = e->v1, c = e->v2;
+    switch (e->code) {
+    case RS16_OK: snprintf(tmp, sizeof tmp, "ok"); break;
+    case RS16_DIFFERENT_SHARD_SIZE:
+        snprintf(tmp, sizeof tmp, "different shard size: expected %llu bytes, got %llu bytes", a, b);
+        break;
+    case RS16_DUPLICATE_ORIGINAL_SHARD_INDEX: snprintf(tmp, sizeof tmp, "duplicate original shard index: %llu", a); break;
+    case RS16_DUPLICATE_RECOVERY_SHARD_INDEX: snprintf(tmp, sizeof tmp, "duplicate recovery shard index: %llu", a); break;
+    case RS16_INVALID_ORIGINAL_SHARD_INDEX:
+        snprintf(tmp, sizeof tmp, "invalid original shard index: %llu >= original_count %llu", b, a);
+        break;
+    case RS16_INVALID_RECOVERY_SHARD_INDEX:
+        snprintf(tmp, sizeof tmp, "invalid recovery shard index: %llu >= recovery_count %llu", b, a);
+        break;
+    case RS16_INVALID_SHARD_SIZE:
+        snprintf(tmp, sizeof tmp, "invalid shard size: %llu bytes (must non-zero and multiple of 64)", a);
+        break;
+    case RS16_NOT_ENOUGH_SHARDS:
+        snprintf(tmp, sizeof tmp, "not enough shards: %llu original + %llu recovery < %llu original_count", b, c, a);
+        break;
+    case RS16_TOO_FEW_ORIGINAL_SHARDS:
+        snprintf(tmp, sizeof tmp, "too few original shards: got %llu shards while original_count is %llu", b, a);
+        break;
+    case RS16_TOO_MANY_ORIGINAL_SHARDS:
+        snprintf(tmp, sizeof tmp, "too many original shards: got more than original_count (%llu) shards", a);
+        break;
+    case RS16_UNSUPPORTED_SHARD_COUNT:
+        snprintf(tmp, sizeof tmp, "unsupported shard count: %llu original shards with %llu recovery shards", a, b);
+        break;
+    case RS16_DEVICE_ERROR: snprintf(tmp, sizeof tmp, "device error: %s", hipGetErrorString((hipError_t)a)); break;
+    case RS16_INVALID_ARGUMENT: snprintf(tmp, sizeof tmp, "invalid argument"); break;
+    default: snprintf(tmp, sizeof tmp, "unknown error %d", e->code); break;
+    }
+    size_t n = strlen(tmp);
+    if (buf && len) {
+        size_t c2 = std::min(n, len - 1);
+        memcpy(buf, tmp, c2);
+        buf[c2] = 0;
+    }
+    return n;
+}
+
+extern "C" void rs16_host_mul(const void* in, void* out, size_t bytes, uint16_t log_m) {
+    const uint32_t* t = &host_tables().mul_tab[(size_t)log_m * TAB_DWORDS];
+    const uint8_t* src = (const uint8_t*)in;
+    uint8_t* dst = (uint8_t*)out;
+    for (size_t q = 0; q < bytes / 8; q++) {
+        const size_t off = (q >> 3) * 64 + (q & 7) * 4;
+        uint32_t yl, yh, ol = 0, oh = 0;
+        memcpy(&yl, src + off, 4);
+        memcpy(&yh, src + off + 32, 4);
+        mul_xor(ol, oh, yl, yh, t);
+        memcpy(dst + off, &ol, 4);
+        memcpy(dst + off + 32, &oh, 4);
+    }
+}
+
+extern "C" int rs16_engine_set_profiling(rs16_engine* e, int enable, rs16_error* err) {
+    if (int rc = e->activate(err)) return rc;
+    if (int rc = e->prof_collect(err)) return rc;
+    e->profiling = enable != 0;
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_profile_read(rs16_engine* e, int prog, double* total_ms, uint64_t* launches,
+                                        rs16_error* err) {
+    if (prog < 0 || prog > NUM_PROGS) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    if (int rc = e->prof_collect(err)) return rc;
+    if (total_ms) *total_ms = e->prof_ms[prog];
+    if (launches) *launches = e->prof_n[prog];
+    return set_error(err, RS16_OK);
+}
+extern "C" void rs16_engine_profile_reset(rs16_engine* e) {
+    rs16_error err;
+    (void)e->activate(&err);
+    (void)e->prof_collect(&err);
+    for (int i = 0; i <= NUM_PROGS; i++) e->prof_ms[i] = 0, e->prof_n[i] = 0;
+}
+extern "C" int rs16_prog_count(void) { return NUM_PROGS + 1; }
+extern "C" const char* rs16_prog_name(int prog) {
+    static const char* names[] = {"GEN_FFT",   "GEN_IFFT",  "ENC_FIRST", "ENC_MID",  "ENC_LAST", "ENC_SINGLE",
+                                  "DEC_FIRST", "DEC_MID",   "DEC_LAST",  "DEC_SINGLE", "EVAL_POLY"};
+    return (prog >= 0 && prog <= NUM_PROGS) ? names[prog] : "?";
+}
+
+extern "C" const char* rs16_version(void) { return "rs16-mi355x 0.1 gfx950 (v_perm GF(2^16) engine)"; }
+
+// ---------------------------------------------------------------------------
+// Rates.
+// ---------------------------------------------------------------------------
+static bool high_supports(size_t k, size_t m) {  // src/rate/rate_high.rs:19-25
+    return k > 0 && m > 0 && k < GF_ORDER && m < GF_ORDER && next_pow2(m) + k <= GF_ORDER;
+}
+static bool low_supports(size_t k, size_t m) {  // src/rate/rate_low.rs:19-25
+    return k > 0 && m > 0 && k < GF_ORDER && m < GF_ORDER && next_pow2(k) + m <= GF_ORDER;
+}
+
+extern "C" int rs16_use_high_rate(size_t k, size_t m, rs16_error* err) {  // rate_default.rs:15-64
+    if (k > GF_ORDER || m > GF_ORDER) return set_error(err, RS16_UNSUPPORTED_SHARD_COUNT, k, m), -1;
+    const size_t kp = next_pow2(k), mp = next_pow2(m);
+    const size_t smaller = std::min(kp, mp), larger = std::max(k, m);
+    if (k == 0 || m == 0 || smaller + larger > GF_ORDER) return set_error(err, RS16_UNSUPPORTED_SHARD_COUNT, k, m), -1;
+    set_error(err, RS16_OK);
+    if (kp < mp) return 0;
+    if (kp > mp) return 1;
+    return k <= m ? 1 : 0;
+}
+
+extern "C" int rs16_supports(int rate, size_t k, size_t m) {
+    if (rate == RS16_RATE_HIGH) return high_supports(k, m);
+    if (rate == RS16_RATE_LOW) return low_supports(k, m);
+    return rs16_use_high_rate(k, m, nullptr) >= 0;
+}
+
+extern "C" int rs16_validate(int rate, size_t k, size_t m, size_t S, rs16_error* err) {  // src/rate.rs:91-106
+    if (!rs16_supports(rate, k, m)) return set_error(err, RS16_UNSUPPORTED_SHARD_COUNT, k, m);
+    if (S == 0 || (S & 63) != 0) return set_error(err, RS16_INVALID_SHARD_SIZE, S);
+    return set_error(err, RS16_OK);
+}
+
+extern "C" size_t rs16_encoder_work_count(int high, size_t k, size_t m) {
+    const size_t chunk = high ? next_pow2(m) : next_pow2(k);
+    const size_t n = high ? k : m;
+    return (n + chunk - 1) / chunk * chunk;
+}
+extern "C" size_t rs16_decoder_work_count(int high, size_t k, size_t m) {
+    return high ? next_pow2(next_pow2(m) + k) : next_pow2(next_pow2(k) + m);
+}
+
+// Resolve the rate of a (rate kind, k, m) request and validate it, the way
+// DefaultRate{En,De}coder::new / reset and {High,Low}Rate*::reset_work do.
+static int resolve_rate(int rate, size_t k, size_t m, size_t S, bool* high, rs16_error* err) {
+    if (rate == RS16_RATE_DEFAULT) {
+        int h = rs16_use_high_rate(k, m, err);
+        if (h < 0) return err ? err->code : RS16_UNSUPPORTED_SHARD_COUNT;
+        *high = h == 1;
+    } else if (rate == RS16_RATE_HIGH || rate == RS16_RATE_LOW) {
+        *high = rate == RS16_RATE_HIGH;
+    } else {
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    }
+    return rs16_validate(*high ? RS16_RATE_HIGH : RS16_RATE_LOW, k, m, S, err);
+}
+
+// ---------------------------------------------------------------------------
+// Engine.
+// ---------------------------------------------------------------------------
+extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
+    int ndev = 0;
+    hipError_t he = hipGetDeviceCount(&ndev);
+    if (he != hipSuccess) return hip_fail(err, he), nullptr;
+    if (device < 0 || device >= ndev) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
+    rs16_engine* e = new (std::nothrow) rs16_engine();
+    if (!e) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
+    e->device = device;
+    const HostTables& t = host_tables();
+    auto fail = [&](hipError_t x) {
+        hip_fail(err, x);
+        rs16_engine_free(e);
+        return (rs16_engine*)nullptr;
+    };
+    if ((he = hipSetDevice(device)) != hipSuccess) return fail(he);
+    if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_skew_entry, t.skew_entry.size() * 4)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_mul_tab, t.mul_tab.size() * 4)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_log_walsh, GF_ORDER * 2)) != hipSuccess) return fail(he);
+    if ((he = hipMemcpy(e->d_skew_entry, t.skew_entry.data(), t.skew_entry.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
+    if ((he = hipMemcpy(e->d_mul_tab, t.mul_tab.data(), t.mul_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
+    if ((he = hipMemcpy(e->d_log_walsh, t.log_walsh.data(), GF_ORDER * 2, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
+    set_error(err, RS16_OK);
+    return e;
+}
+
+extern "C" void rs16_engine_free(rs16_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    e->ws_z.release();
+    e->ws_u.release();
+    e->ws_fd.release();
+    e->ws_work32.release();
+    e->ws_elog.release();
+    e->ws_flags.release();
+    if (e->d_skew_entry) (void)hipFree(e->d_skew_entry);
+    if (e->d_mul_tab) (void)hipFree(e->d_mul_tab);
+    if (e->d_log_walsh) (void)hipFree(e->d_log_walsh);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+extern "C" int rs16_engine_device(const rs16_engine* e) { return e->device; }
+extern "C" void* rs16_engine_stream(const rs16_engine* e) { return (void*)e->stream; }
+extern "C" int rs16_engine_synchronize(rs16_engine* e, void* stream, rs16_error* err) {
+    if (int rc = e->activate(err)) return rc;
+    RS16_HIP(hipStreamSynchronize(e->pick(stream)));
+    return set_error(err, RS16_OK);
+}
+
+// ---- engine ops -----------------------------------------------------------
+static bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
+
+static int check_transform(size_t shard_count, size_t S, size_t pos, size_t size, size_t trunc, size_t skew_delta,
+                           rs16_error* err) {
+    if (S == 0 || (S & 63) || !is_pow2(size) || size > GF_ORDER || trunc > size || pos + size > shard_count)
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    // largest twiddle index touched: (size - 2) + skew_delta must be < GF_MODULUS
+    if (size >= 2 && size - 2 + skew_delta >= GF_MODULUS) return set_error(err, RS16_INVALID_ARGUMENT);
+    return RS16_OK;
+}
+
+extern "C" int rs16_engine_fft(rs16_engine* e, void* data, size_t shard_count, size_t S, size_t pos, size_t size,
+                               size_t trunc, size_t skew_delta, void* stream, rs16_error* err) {
+    if (int rc = check_transform(shard_count, S, pos, size, trunc, skew_delta, err)) return rc;
+    if (int rc = e->activate(err)) return rc;
+    if (int rc = e->fft((uint8_t*)data, S, pos, size, skew_delta, e->pick(stream), err)) return rc;
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_fft_skew_end(rs16_engine* e, void* data, size_t shard_count, size_t S, size_t pos,
+                                        size_t size, size_t trunc, void* stream, rs16_error* err) {
+    return rs16_engine_fft(e, data, shard_count, S, pos, size, trunc, pos + size, stream, err);
+}
+extern "C" int rs16_engine_ifft(rs16_engine* e, void* data, size_t shard_count, size_t S, size_t pos, size_t size,
+                                size_t trunc, size_t skew_delta, void* stream, rs16_error* err) {
+    if (int rc = check_transform(shard_count, S, pos, size, trunc, skew_delta, err)) return rc;
+    if (int rc = e->activate(err)) return rc;
+    if (int rc = e->ifft((uint8_t*)data, S, pos, size, skew_delta, e->pick(stream), err)) return rc;
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_ifft_skew_end(rs16_engine* e, void* data, size_t shard_count, size_t S, size_t pos,
+                                         size_t size, size_t trunc, void* stream, rs16_error* err) {
+    return rs16_engine_ifft(e, data, shard_count, S, pos, size, trunc, pos + size, stream, err);
+}
+extern "C" int rs16_engine_fwht(rs16_engine* e, uint16_t* d, size_t trunc, void* stream, rs16_error* err) {
+    if (trunc > GF_ORDER) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
+    RS16_HIP(launch_fwht_u16(d, (uint32_t*)e->ws_work32.p, e->pick(stream)));
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_eval_poly(rs16_engine* e, uint16_t* d, size_t trunc, void* stream, rs16_error* err) {
+    if (trunc > GF_ORDER) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
+    RS16_HIP(launch_eval_poly_u16(d, (uint32_t*)e->ws_work32.p, e->d_log_walsh, e->pick(stream)));
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_mul(rs16_engine* e, void* x, size_t bytes, uint16_t log_m, void* stream, rs16_error* err) {
+    if (bytes & 63) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    RS16_HIP(launch_mul((uint8_t*)x, bytes, log_m, e->d_mul_tab, e->pick(stream)));
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_xor(rs16_engine* e, void* x, const void* y, size_t bytes, void* stream, rs16_error* err) {
+    if (bytes & 63) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    RS16_HIP(launch_xor((uint8_t*)x, (const uint8_t*)y, bytes, e->pick(stream)));
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_xor_within(rs16_engine* e, void* data, size_t shard_count, size_t S, size_t x, size_t y,
+                                      size_t count, void* stream, rs16_error* err) {
+    if ((S & 63) || x + count > shard_count || y + count > shard_count || (x < y ? x + count > y : y + count > x))
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    uint8_t* d = (uint8_t*)data;
+    return rs16_engine_xor(e, d + x * S, d + y * S, count * S, stream, err);
+}
+extern "C" int rs16_engine_formal_derivative(rs16_engine* e, void* data, size_t n, size_t S, void* stream,
+                                             rs16_error* err) {
+    if ((S & 63) || S == 0 || !is_pow2(n)) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    RS16_HIP(e->ws_fd.reserve(n * S));
+    RS16_HIP(launch_formal_derivative((uint8_t*)e->ws_fd.p, (const uint8_t*)data, n, S, s));
+    RS16_HIP(hipMemcpyAsync(data, e->ws_fd.p, n * S, hipMemcpyDeviceToDevice, s));
+    return set_error(err, RS16_OK);
+}
+
+// ---------------------------------------------------------------------------
+// Encoder -- EncoderWork (src/rate/encoder_work.rs) + Rate encoders.
+// ---------------------------------------------------------------------------
+struct rs16_encoder {
+    rs16_engine* eng;
+    int rate_kind;
+    bool high = true;
+    size_t k = 0, m = 0, S = 0, work_count = 0, received = 0;
+    DevBuf work;
+};
+
+static int encoder_reset_impl(rs16_encoder* enc, size_t k, size_t m, size_t S, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(enc->rate_kind, k, m, S, &high, err)) return rc;
+    const size_t wc = rs16_encoder_work_count(high, k, m);
+    if (int rc = enc->eng->activate(err)) return rc;
+    RS16_HIP(enc->work.reserve(wc * S));
+    enc->high = high;
+    enc->k = k;
+    enc->m = m;
+    enc->S = S;
+    enc->work_count = wc;
+    enc->received = 0;
+    return set_error(err, RS16_OK);
+}
+
+extern "C" rs16_encoder* rs16_encoder_new(rs16_engine* eng, int rate, size_t k, size_t m, size_t S, rs16_error* err) {
+    rs16_encoder* enc = new (std::nothrow) rs16_encoder();
+    if (!enc) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
+    enc->eng = eng;
+    enc->rate_kind = rate;
+    if (encoder_reset_impl(enc, k, m, S, err)) {
+        rs16_encoder_free(enc);
+        return nullptr;
+    }
+    return enc;
+}
+extern "C" void rs16_encoder_free(rs16_encoder* enc) {
+    if (!enc) return;
+    (void)hipSetDevice(enc->eng->device);
+    (void)hipStreamSynchronize(enc->eng->stream);
+    enc->work.release();
+    delete enc;
+}
+extern "C" int rs16_encoder_reset(rs16_encoder* enc, size_t k, size_t m, size_t S, rs16_error* err) {
+    return encoder_reset_impl(enc, k, m, S, err);
+}
+static int encoder_add(rs16_encoder* enc, const void* shard, size_t len, bool device, rs16_error* err) {
+    if (enc->received == enc->k) return set_error(err, RS16_TOO_MANY_ORIGINAL_SHARDS, enc->k);
+    if (len != enc->S) return set_error(err, RS16_DIFFERENT_SHARD_SIZE, enc->S, len);
+    if (int rc = enc->eng->activate(err)) return rc;
+    uint8_t* dst = (uint8_t*)enc->work.p + enc->received * enc->S;
+    if (device) RS16_HIP(hipMemcpyAsync(dst, shard, len, hipMemcpyDeviceToDevice, enc->eng->stream));
+    else RS16_HIP(hipMemcpyAsync(dst, shard, len, hipMemcpyHostToDevice, enc->eng->stream));
+    if (!device) RS16_HIP(hipStreamSynchronize(enc->eng->stream));  // the caller may reuse its buffer
+    enc->received++;
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_encoder_add_original_shard(rs16_encoder* enc, const void* shard, size_t len, rs16_error* err) {
+    return encoder_add(enc, shard, len, false, err);
+}
+extern "C" int rs16_encoder_add_original_shard_device(rs16_encoder* enc, const void* d, size_t len, rs16_error* err) {
+    return encoder_add(enc, d, len, true, err);
+}
+extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
+    if (enc->received != enc->k) return set_error(err, RS16_TOO_FEW_ORIGINAL_SHARDS, enc->k, enc->received);
+    rs16_engine* e = enc->eng;
+    if (int rc = e->activate(err)) return rc;
+    uint8_t* w = (uint8_t*)enc->work.p;
+    const size_t chunk = next_pow2(enc->m);
+    int rc;
+    if (enc->high && enc->k <= chunk)
+        rc = e->encode_high_fused(enc->k, enc->m, enc->S, w, w, w, e->stream, err);
+    else if (enc->high)
+        rc = e->encode_high_generic(enc->k, enc->m, enc->S, w, enc->work_count, e->stream, err);
+    else
+        rc = e->encode_low_generic(enc->k, enc->m, enc->S, w, enc->work_count, e->stream, err);
+    if (rc) return rc;
+    return set_error(err, RS16_OK);
+}
+extern "C" const void* rs16_encoder_recovery_device(rs16_encoder* enc, size_t index) {
+    return index < enc->m ? (const uint8_t*)enc->work.p + index * enc->S : nullptr;
+}
+extern "C" int rs16_encoder_recovery_copy(rs16_encoder* enc, size_t index, void* dst, size_t len, rs16_error* err) {
+    const void* src = rs16_encoder_recovery_device(enc, index);
+    if (!src) return set_error(err, RS16_OK), 0;
+    if (len < enc->S) return set_error(err, RS16_INVALID_ARGUMENT), -1;
+    if (enc->eng->activate(err)) return -1;
+    hipError_t he = hipMemcpyAsync(dst, src, enc->S, hipMemcpyDeviceToHost, enc->eng->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(enc->eng->stream);
+    if (he != hipSuccess) return hip_fail(err, he), -1;
+    return set_error(err, RS16_OK), 1;
+}
+extern "C" void rs16_encoder_result_drop(rs16_encoder* enc) { enc->received = 0; }
+extern "C" int rs16_encoder_is_high_rate(const rs16_encoder* enc) { return enc->high; }
+
+// ---------------------------------------------------------------------------
+// Decoder -- DecoderWork (src/rate/decoder_work.rs) + Rate decoders.
+// ---------------------------------------------------------------------------
+struct rs16_decoder {
+    rs16_engine* eng;
+    int rate_kind;
+    bool high = true;
+    size_t k = 0, m = 0, S = 0, work_count = 0;
+    size_t orig_base = 0, rec_base = 0, orig_recv = 0, rec_recv = 0;
+    std::vector<uint8_t> received;  // by work position
+    DevBuf work, ubuf, flags;       // work = shards (z), ubuf = second work array (u)
+};
+
+static int decoder_reset_impl(rs16_decoder* d, size_t k, size_t m, size_t S, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(d->rate_kind, k, m, S, &high, err)) return rc;
+    const size_t wc = rs16_decoder_work_count(high, k, m);
+    if (int rc = d->eng->activate(err)) return rc;
+    RS16_HIP(d->work.reserve(wc * S));
+    RS16_HIP(d->ubuf.reserve(wc * S));
+    RS16_HIP(d->flags.reserve(GF_ORDER * 2));
+    d->high = high;
+    d->k = k;
+    d->m = m;
+    d->S = S;
+    d->work_count = wc;
+    d->orig_base = high ? next_pow2(m) : 0;  // rate_high.rs:279-299 / rate_low.rs:279-299
+    d->rec_base = high ? 0 : next_pow2(k);
+    d->orig_recv = d->rec_recv = 0;
+    d->received.assign(std::max(d->received.size(), wc), 0);
+    return set_error(err, RS16_OK);
+}
+
+extern "C" rs16_decoder* rs16_decoder_new(rs16_engine* eng, int rate, size_t k, size_t m, size_t S, rs16_error* err) {
+    rs16_decoder* d = new (std::nothrow) rs16_decoder();
+    if (!d) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
+    d->eng = eng;
+    d->rate_kind = rate;
+    if (decoder_reset_impl(d, k, m, S, err)) {
+        rs16_decoder_free(d);
+        return nullptr;
+    }
+    return d;
+}
+extern "C" void rs16_decoder_free(rs16_decoder* d) {
+    if (!d) return;
+    (void)hipSetDevice(d->eng->device);
+    (void)hipStreamSynchronize(d->eng->stream);
+    d->work.release();
+    d->ubuf.release();
+    d->flags.release();
+    delete d;
+}
+extern "C" int rs16_decoder_reset(rs16_decoder* d, size_t k, size_t m, size_t S, rs16_error* err) {
+    return decoder_reset_impl(d, k, m, S, err);
+}
+static int decoder_add(rs16_decoder* d, bool original, size_t index, const void* shard, size_t len, bool device,
+                       rs16_error* err) {
+    const size_t count = original ? d->k : d->m;
+    const size_t pos = (original ? d->orig_base : d->rec_base) + index;
+    if (index >= count)
+        return set_error(err, original ? RS16_INVALID_ORIGINAL_SHARD_INDEX : RS16_INVALID_RECOVERY_SHARD_INDEX, count,
+                         index);
+    if (d->received[pos])
+        return set_error(err, original ? RS16_DUPLICATE_ORIGINAL_SHARD_INDEX : RS16_DUPLICATE_RECOVERY_SHARD_INDEX,
+                         index);
+    if (len != d->S) return set_error(err, RS16_DIFFERENT_SHARD_SIZE, d->S, len);
+    if (int rc = d->eng->activate(err)) return rc;
+    uint8_t* dst = (uint8_t*)d->work.p + pos * d->S;
+    RS16_HIP(hipMemcpyAsync(dst, shard, len, device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, d->eng->stream));
+    if (!device) RS16_HIP(hipStreamSynchronize(d->eng->stream));
+    (original ? d->orig_recv : d->rec_recv)++;
+    d->received[pos] = 1;
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_decoder_add_original_shard(rs16_decoder* d, size_t i, const void* s, size_t len, rs16_error* err) {
+    return decoder_add(d, true, i, s, len, false, err);
+}
+extern "C" int rs16_decoder_add_recovery_shard(rs16_decoder* d, size_t i, const void* s, size_t len, rs16_error* err) {
+    return decoder_add(d, false, i, s, len, false, err);
+}
+extern "C" int rs16_decoder_add_original_shard_device(rs16_decoder* d, size_t i, const void* s, size_t len,
+                                                      rs16_error* err) {
+    return decoder_add(d, true, i, s, len, true, err);
+}
+extern "C" int rs16_decoder_add_recovery_shard_device(rs16_decoder* d, size_t i, const void* s, size_t len,
+                                                      rs16_error* err) {
+    return decoder_add(d, false, i, s, len, true, err);
+}
+extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
+    // decode_begin (src/rate/decoder_work.rs:120-139)
+    if (d->orig_recv + d->rec_recv < d->k)
+        return set_error(err, RS16_NOT_ENOUGH_SHARDS, d->k, d->orig_recv, d->rec_recv);
+    if (d->orig_recv == d->k) return set_error(err, RS16_OK);  // nothing to do
+    rs16_engine* e = d->eng;
+    if (int rc = e->activate(err)) return rc;
+    const DecodeGeom g = decode_geom(d->high, d->k, d->m);
+    // Received flags of the two segments -> device (bytes, one per row).
+    uint8_t* fl = (uint8_t*)d->flags.p;
+    RS16_HIP(hipMemcpyAsync(fl, d->received.data(), g.a_count, hipMemcpyHostToDevice, e->stream));
+    RS16_HIP(hipMemcpyAsync(fl + GF_ORDER, d->received.data() + g.chunk, g.b_count, hipMemcpyHostToDevice, e->stream));
+    uint8_t* w = (uint8_t*)d->work.p;
+    if (int rc = e->decode_fused(g, d->S, w, fl, w + (size_t)g.chunk * d->S, fl + GF_ORDER, w + d->orig_base * d->S,
+                                 w, (uint8_t*)d->ubuf.p, e->stream, err))
+        return rc;
+    RS16_HIP(hipStreamSynchronize(e->stream));  // host flag buffers are pageable
+    return set_error(err, RS16_OK);
+}
+extern "C" const void* rs16_decoder_restored_original_device(rs16_decoder* d, size_t index) {
+    const size_t pos = d->orig_base + index;
+    if (index < d->k && !d->received[pos]) return (const uint8_t*)d->work.p + pos * d->S;
+    return nullptr;
+}
+extern "C" int rs16_decoder_restored_original_copy(rs16_decoder* d, size_t index, void* dst, size_t len,
+                                                   rs16_error* err) {
+    const void* src = rs16_decoder_restored_original_device(d, index);
+    if (!src) return set_error(err, RS16_OK), 0;
+    if (len < d->S) return set_error(err, RS16_INVALID_ARGUMENT), -1;
+    if (d->eng->activate(err)) return -1;
+    hipError_t he = hipMemcpyAsync(dst, src, d->S, hipMemcpyDeviceToHost, d->eng->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(d->eng->stream);
+    if (he != hipSuccess) return hip_fail(err, he), -1;
+    return set_error(err, RS16_OK), 1;
+}
+extern "C" void rs16_decoder_result_drop(rs16_decoder* d) {  // DecoderWork::reset_received
+    d->orig_recv = d->rec_recv = 0;
+    std::fill(d->received.begin(), d->received.end(), 0);
+}
+extern "C" int rs16_decoder_is_high_rate(const rs16_decoder* d) { return d->high; }
+
+// ---------------------------------------------------------------------------
+// Device-resident one-shot codec.
+// ---------------------------------------------------------------------------
+extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, const void* d_original,
+                                  void* d_recovery, void* stream, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    const size_t wc = rs16_encoder_work_count(high, k, m);
+    RS16_HIP(e->ws_z.reserve(wc * S));
+    uint8_t* Z = (uint8_t*)e->ws_z.p;
+    int rc;
+    if (high && k <= next_pow2(m)) {
+        rc = e->encode_high_fused(k, m, S, (const uint8_t*)d_original, (uint8_t*)d_recovery, Z, s, err);
+    } else {
+        RS16_HIP(hipMemcpyAsync(Z, d_original, k * S, hipMemcpyDeviceToDevice, s));
+        rc = high ? e->encode_high_generic(k, m, S, Z, wc, s, err) : e->encode_low_generic(k, m, S, Z, wc, s, err);
+        if (!rc) RS16_HIP(hipMemcpyAsync(d_recovery, Z, m * S, hipMemcpyDeviceToDevice, s));
+    }
+    if (rc) return rc;
+    return set_error(err, RS16_OK);
+}
+
+extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, void* d_original,
+                                  const uint8_t* d_original_received, const void* d_recovery,
+                                  const uint8_t* d_recovery_received, size_t orig_recv, size_t rec_recv, void* stream,
+                                  rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
+    if (orig_recv == k) return set_error(err, RS16_OK);
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    const DecodeGeom g = decode_geom(high, k, m);
+    RS16_HIP(e->ws_z.reserve((size_t)g.n * S));
+    RS16_HIP(e->ws_u.reserve((size_t)g.n * S));
+    const uint8_t* orig = (const uint8_t*)d_original;
+    const uint8_t* rec = (const uint8_t*)d_recovery;
+    int rc = high ? e->decode_fused(g, S, rec, d_recovery_received, orig, d_original_received, (uint8_t*)d_original,
+                                    (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p, s, err)
+                  : e->decode_fused(g, S, orig, d_original_received, rec, d_recovery_received, (uint8_t*)d_original,
+                                    (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p, s, err);
+    if (rc) return rc;
+    return set_error(err, RS16_OK);
+}
+
+// ---------------------------------------------------------------------------
+// Device memory helpers.
+// ---------------------------------------------------------------------------
+extern "C" void* rs16_device_alloc(rs16_engine* e, size_t bytes, rs16_error* err) {
+    if (e->activate(err)) return nullptr;
+    void* p = nullptr;
+    hipError_t he = hipMalloc(&p, bytes ? bytes : 1);
+    if (he != hipSuccess) return hip_fail(err, he), nullptr;
+    set_error(err, RS16_OK);
+    return p;
+}
+extern "C" void rs16_device_free(rs16_engine* e, void* p) {
+    if (!p) return;
+    (void)hipSetDevice(e->device);
+    (void)hipFree(p);
+}
+extern "C" int rs16_memcpy_htod(rs16_engine* e, void* dst, const void* src, size_t bytes, void* stream,
+                                rs16_error* err) {
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    RS16_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    RS16_HIP(hipStreamSynchronize(s));
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_memcpy_dtoh(rs16_engine* e, void* dst, const void* src, size_t bytes, void* stream,
+                                rs16_error* err) {
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    RS16_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    RS16_HIP(hipStreamSynchronize(s));
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_memset_device(rs16_engine* e, void* dst, int value, size_t bytes, void* stream, rs16_error* err) {
+    if (int rc = e->activate(err)) return rc;
+    RS16_HIP(hipMemsetAsync(dst, value, bytes, e->pick(stream)));
+    return set_error(err, RS16_OK);
+}

@@ -1,0 +1,303 @@
+// rs16_engine.cpp -- engine object: tables in HBM, engine-level transforms
+// as HBM passes, and the fused encode/decode pass sequences.
+#include "rs16_engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace rs16 {
+
+hipError_t DevBuf::reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+int set_error(rs16_error* err, int code, uint64_t v0, uint64_t v1, uint64_t v2) {
+    if (err) {
+        err->code = code;
+        err->v0 = v0;
+        err->v1 = v1;
+        err->v2 = v2;
+    }
+    return code;
+}
+int hip_fail(rs16_error* err, hipError_t e) { return set_error(err, RS16_DEVICE_ERROR, (uint64_t)e); }
+
+size_t next_pow2(size_t x) {
+    size_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+DecodeGeom decode_geom(bool high, size_t k, size_t m) {
+    DecodeGeom g;
+    g.high = high;
+    g.a_count = (uint32_t)(high ? m : k);
+    g.b_count = (uint32_t)(high ? k : m);
+    g.chunk = (uint32_t)next_pow2(g.a_count);
+    g.n = (uint32_t)next_pow2((size_t)g.chunk + g.b_count);
+    return g;
+}
+
+static PassArgs base_args(const rs16_engine* e, size_t S) {
+    PassArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.skew_entry = e->d_skew_entry;
+    a.mul_tab = e->d_mul_tab;
+    a.S = S;
+    a.qrow = (uint32_t)(S / 8);
+    a.nslab = (a.qrow + 63) / 64;
+    return a;
+}
+
+}  // namespace rs16
+
+using namespace rs16;
+
+int rs16_engine::activate(rs16_error* err) {
+    RS16_HIP(hipSetDevice(device));
+    return RS16_OK;
+}
+
+int rs16_engine::prof_begin(hipStream_t s, hipEvent_t* ev, rs16_error* err) {
+    *ev = nullptr;
+    if (!profiling) return RS16_OK;
+    if (ev_pool.empty()) {
+        hipEvent_t e;
+        RS16_HIP(hipEventCreate(&e));
+        ev_pool.push_back(e);
+    }
+    *ev = ev_pool.back();
+    ev_pool.pop_back();
+    RS16_HIP(hipEventRecord(*ev, s));
+    return RS16_OK;
+}
+
+int rs16_engine::prof_end(int id, hipStream_t s, hipEvent_t ev, rs16_error* err) {
+    if (!ev) return RS16_OK;
+    if (ev_pool.empty()) {
+        hipEvent_t e;
+        RS16_HIP(hipEventCreate(&e));
+        ev_pool.push_back(e);
+    }
+    hipEvent_t b = ev_pool.back();
+    ev_pool.pop_back();
+    RS16_HIP(hipEventRecord(b, s));
+    prof_pending.push_back({id, ev, b});
+    if (prof_pending.size() > 4096) return prof_collect(err);  // bound the event pool
+    return RS16_OK;
+}
+
+int rs16_engine::prof_collect(rs16_error* err) {
+    for (const ProfRec& r : prof_pending) {
+        RS16_HIP(hipEventSynchronize(r.b));
+        float ms = 0.f;
+        RS16_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+        prof_ms[r.id] += ms;
+        prof_n[r.id] += 1;
+        ev_pool.push_back(r.a);
+        ev_pool.push_back(r.b);
+    }
+    prof_pending.clear();
+    return RS16_OK;
+}
+
+int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStream_t s, rs16_error* err) {
+    hipEvent_t ev;
+    if (int rc = prof_begin(s, &ev, err)) return rc;
+    RS16_HIP(launch_pass(prog, T, a, tiles, s));
+    return prof_end(prog, s, ev, err);
+}
+
+// Engine::fft over 2^L rows: L <= 8 in one pass; otherwise the high
+// (L - L/2) row bits as a strided pass, then the low L/2 bits contiguous.
+int rs16_engine::fft(uint8_t* data, size_t S, size_t pos, size_t size, size_t skew_delta, hipStream_t s,
+                     rs16_error* err) {
+    const int L = ilog2(size);
+    if (L == 0) return RS16_OK;
+    PassArgs a = base_args(this, S);
+    a.in = a.out = data + pos * S;
+    a.skew_fft = (uint32_t)skew_delta;
+    if (L <= 8) {
+        RS16_PASS(GEN_FFT, L, a, 1, s);
+        return RS16_OK;
+    }
+    const int lo = L / 2, hi = L - lo;
+    a.lo = lo;
+    RS16_PASS(GEN_FFT, hi, a, 1u << lo, s);
+    a.lo = 0;
+    RS16_PASS(GEN_FFT, lo, a, 1u << hi, s);
+    return RS16_OK;
+}
+
+int rs16_engine::ifft(uint8_t* data, size_t S, size_t pos, size_t size, size_t skew_delta, hipStream_t s,
+                      rs16_error* err) {
+    const int L = ilog2(size);
+    if (L == 0) return RS16_OK;
+    PassArgs a = base_args(this, S);
+    a.in = a.out = data + pos * S;
+    a.skew_ifft = (uint32_t)skew_delta;
+    if (L <= 8) {
+        RS16_PASS(GEN_IFFT, L, a, 1, s);
+        return RS16_OK;
+    }
+    const int lo = L / 2, hi = L - lo;
+    a.lo = 0;
+    RS16_PASS(GEN_IFFT, lo, a, 1u << hi, s);
+    a.lo = lo;
+    RS16_PASS(GEN_IFFT, hi, a, 1u << lo, s);
+    return RS16_OK;
+}
+
+// HighRateEncoder::encode for original_count <= chunk (src/rate/rate_high.rs:44-83):
+//   recovery = FFT(IFFT(originals zero-padded to chunk, skew = chunk), skew = 0)[0..m)
+// as three passes over the 2-D row factorisation (contiguous low bits /
+// strided high bits); IFFT-high and FFT-high share the strided pass.
+int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
+                                   hipStream_t s, rs16_error* err) {
+    const size_t chunk = next_pow2(m);
+    const int L = ilog2(chunk);
+    PassArgs a = base_args(this, S);
+    a.seg_a = d_orig;
+    a.a_count = (uint32_t)k;
+    a.skew_ifft = (uint32_t)chunk;
+    a.skew_fft = 0;
+    a.out_rows = (uint32_t)m;
+    if (L <= 8) {
+        a.out = d_rec;
+        RS16_PASS(ENC_SINGLE, L, a, 1, s);
+        return RS16_OK;
+    }
+    const int lo = L / 2, hi = L - lo;
+    a.out = Z;
+    a.lo = 0;
+    RS16_PASS(ENC_FIRST, lo, a, 1u << hi, s);
+    a.in = Z;
+    a.lo = lo;
+    RS16_PASS(ENC_MID, hi, a, 1u << lo, s);
+    a.in = Z;
+    a.out = d_rec;
+    a.lo = 0;
+    const uint32_t tiles = (uint32_t)((m + ((size_t)1 << lo) - 1) >> lo);
+    RS16_PASS(ENC_LAST, lo, a, tiles, s);
+    return RS16_OK;
+}
+
+// {High,Low}RateDecoder::decode (src/rate/rate_high.rs:168-247,
+// src/rate/rate_low.rs:168-247), all in HBM:
+//   e     = eval_poly(erasure vector)                       (3 small kernels)
+//   z     = IFFT_low(received * e)                          (pass 1, contiguous)
+//   u     = FFT_high((I + H) IFFT_high(z))                  (pass 2, strided)
+//   y     = u + L z,  out = reveal(FFT_low(y))              (pass 3, contiguous)
+// where the formal derivative FD = I + L + H is split into its low-bit part L
+// and high-bit part H (L commutes with the high-bit layers and
+// FFT_high o IFFT_high = I), so no separate derivative pass is needed.
+int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+                              const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
+                              hipStream_t s, rs16_error* err) {
+    RS16_HIP(ws_work32.reserve(GF_ORDER * 4));
+    RS16_HIP(ws_elog.reserve(GF_ORDER * 4));
+    ErasureSpec es;
+    es.flags_a = flags_a;
+    es.flags_b = flags_b;
+    es.a_count = g.a_count;
+    es.chunk = g.chunk;
+    es.b_count = g.b_count;
+    es.pad_fill = g.high ? 1 : 0;
+    es.tail_fill = g.high ? 0 : 1;
+    hipEvent_t ev;
+    if (int rc = prof_begin(s, &ev, err)) return rc;
+    RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s));
+    if (int rc = prof_end(NUM_PROGS, s, ev, err)) return rc;
+
+    PassArgs a = base_args(this, S);
+    a.seg_a = seg_a;
+    a.seg_b = seg_b;
+    a.flags_a = flags_a;
+    a.flags_b = flags_b;
+    a.a_count = g.a_count;
+    a.chunk = g.chunk;
+    a.b_count = g.b_count;
+    a.elog = (const uint32_t*)ws_elog.p;
+    a.rest = rest;
+    a.rest_seg_b = g.high ? 1 : 0;
+    a.skew_ifft = a.skew_fft = 0;
+    const int L = ilog2(g.n);
+    if (L <= 8) {
+        RS16_PASS(DEC_SINGLE, L, a, 1, s);
+        return RS16_OK;
+    }
+    const int lo = L / 2, hi = L - lo;
+    a.lo = 0;
+    a.out = Z;
+    RS16_PASS(DEC_FIRST, lo, a, 1u << hi, s);
+    a.lo = lo;
+    a.in = Z;
+    a.out = U;
+    RS16_PASS(DEC_MID, hi, a, 1u << lo, s);
+    // Only tiles that contain original rows are needed in the last pass.
+    const uint32_t ob = g.high ? g.chunk : 0;
+    const uint32_t oc = g.high ? g.b_count : g.a_count;
+    const uint32_t t0 = ob >> lo, t1 = (uint32_t)(((size_t)ob + oc + ((size_t)1 << lo) - 1) >> lo);
+    a.lo = 0;
+    a.in = Z;
+    a.in2 = U;
+    a.out = nullptr;
+    a.tile_base = t0;
+    RS16_PASS(DEC_LAST, lo, a, t1 - t0, s);
+    return RS16_OK;
+}
+
+// HighRateEncoder::encode, general case (src/rate/rate_high.rs:44-83).
+int rs16_engine::encode_high_generic(size_t k, size_t m, size_t S, uint8_t* w, size_t work_count, hipStream_t s,
+                                     rs16_error* err) {
+    const size_t chunk = next_pow2(m);
+    const size_t first = std::min(k, chunk);
+    if (chunk > first) RS16_HIP(hipMemsetAsync(w + first * S, 0, (chunk - first) * S, s));
+    if (int rc = ifft(w, S, 0, chunk, chunk, s, err)) return rc;
+    if (k > chunk) {
+        size_t cs = chunk;
+        while (cs + chunk <= k) {
+            if (int rc = ifft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
+            RS16_HIP(launch_xor(w, w + cs * S, chunk * S, s));
+            cs += chunk;
+        }
+        const size_t last = k % chunk;
+        if (last > 0) {
+            RS16_HIP(hipMemsetAsync(w + (cs + last) * S, 0, (work_count - cs - last) * S, s));
+            if (int rc = ifft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
+            RS16_HIP(launch_xor(w, w + cs * S, chunk * S, s));
+        }
+    }
+    return fft(w, S, 0, chunk, 0, s, err);
+}
+
+// LowRateEncoder::encode (src/rate/rate_low.rs:44-83).
+int rs16_engine::encode_low_generic(size_t k, size_t m, size_t S, uint8_t* w, size_t work_count, hipStream_t s,
+                                    rs16_error* err) {
+    (void)work_count;
+    const size_t chunk = next_pow2(k);
+    if (chunk > k) RS16_HIP(hipMemsetAsync(w + k * S, 0, (chunk - k) * S, s));
+    if (int rc = ifft(w, S, 0, chunk, 0, s, err)) return rc;
+    for (size_t cs = chunk; cs < m; cs += chunk)
+        RS16_HIP(hipMemcpyAsync(w + cs * S, w, chunk * S, hipMemcpyDeviceToDevice, s));
+    size_t cs = 0;
+    while (cs + chunk <= m) {
+        if (int rc = fft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
+        cs += chunk;
+    }
+    if (m % chunk) {
+        if (int rc = fft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
+    }
+    return RS16_OK;
+}

@@ -1,0 +1,93 @@
+// rs16_engine.hpp -- host-side engine object and pass drivers (internal).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rs16.h"
+#include "rs16_internal.hpp"
+
+namespace rs16 {
+
+// Grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes);
+    void release();
+};
+
+// Status helper: every internal call returns an rs16 code and fills err.
+int set_error(rs16_error* err, int code, uint64_t v0 = 0, uint64_t v1 = 0, uint64_t v2 = 0);
+int hip_fail(rs16_error* err, hipError_t e);
+#define RS16_HIP(call)                                 \
+    do {                                               \
+        hipError_t _e = (call);                        \
+        if (_e != hipSuccess) return hip_fail(err, _e); \
+    } while (0)
+#define RS16_PASS(...)                                       \
+    do {                                                     \
+        if (int _rc = this->pass(__VA_ARGS__, err)) return _rc; \
+    } while (0)
+
+size_t next_pow2(size_t x);
+inline int ilog2(size_t x) { int l = 0; while (((size_t)1 << l) < x) l++; return l; }
+
+// Geometry of a decode (both rates): segment A = rows [0, a_count),
+// segment B = rows [chunk, chunk + b_count), transform of n rows.
+struct DecodeGeom {
+    bool high;
+    uint32_t a_count, chunk, b_count, n;
+};
+DecodeGeom decode_geom(bool high, size_t k, size_t m);
+
+}  // namespace rs16
+
+struct rs16_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t* d_skew_entry = nullptr;
+    uint32_t* d_mul_tab = nullptr;
+    uint16_t* d_log_walsh = nullptr;
+    // scratch
+    rs16::DevBuf ws_z, ws_u, ws_fd, ws_work32, ws_elog, ws_flags;
+
+    hipStream_t pick(void* s) const { return s ? (hipStream_t)s : stream; }
+    int activate(rs16_error* err);
+
+    // Pass launch (with optional per-program hipEvent timing on the launch
+    // stream; id NUM_PROGS = the eval_poly kernels of a decode).
+    int pass(int prog, int T, const rs16::PassArgs& a, uint32_t tiles, hipStream_t s, rs16_error* err);
+    int prof_begin(hipStream_t s, hipEvent_t* ev, rs16_error* err);
+    int prof_end(int id, hipStream_t s, hipEvent_t ev, rs16_error* err);
+    bool profiling = false;
+    struct ProfRec {
+        int id;
+        hipEvent_t a, b;
+    };
+    std::vector<ProfRec> prof_pending;
+    std::vector<hipEvent_t> ev_pool;
+    double prof_ms[rs16::NUM_PROGS + 1] = {};
+    uint64_t prof_n[rs16::NUM_PROGS + 1] = {};
+    int prof_collect(rs16_error* err);
+
+    // Engine ops on device shard arrays (validated by the C ABI layer).
+    int fft(uint8_t* data, size_t S, size_t pos, size_t size, size_t skew_delta, hipStream_t s, rs16_error* err);
+    int ifft(uint8_t* data, size_t S, size_t pos, size_t size, size_t skew_delta, hipStream_t s, rs16_error* err);
+
+    // Fused HighRate single-chunk encode: originals rows [0,k) of d_orig ->
+    // recovery rows [0,m) of d_rec, using Z (chunk rows) as work.
+    int encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
+                          hipStream_t s, rs16_error* err);
+    // Fused decode (both rates): seg_a / seg_b gather sources with device
+    // flags; lost originals written to rest; Z, U work (n rows each; Z may
+    // alias the sources when they live at their work positions).
+    int decode_fused(const rs16::DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+                     const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
+                     hipStream_t s, rs16_error* err);
+    // Generic (engine-op sequence) encoders, following the reference rate code.
+    int encode_high_generic(size_t k, size_t m, size_t S, uint8_t* work, size_t work_count, hipStream_t s,
+                            rs16_error* err);
+    int encode_low_generic(size_t k, size_t m, size_t S, uint8_t* work, size_t work_count, hipStream_t s,
+                           rs16_error* err);
+};

@@ -1,0 +1,86 @@
+// rs16_internal.hpp -- shared declarations of the MI355X engine (not part of
+// the public C ABI; see include/rs16.h for that).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "rs16_gf.hpp"
+
+namespace rs16 {
+
+struct HostTables {
+    std::vector<uint16_t> exp, log, skew, log_walsh;
+    std::vector<uint32_t> skew_entry;  // GF_ORDER entries: mul-table entry of each twiddle
+    std::vector<uint32_t> mul_tab;     // TAB_ENTRIES * TAB_DWORDS
+};
+const HostTables& host_tables();
+
+// ---------------------------------------------------------------------------
+// Pass kernels.  A "pass" applies a contiguous range of FFT/IFFT layers to
+// tiles of 2^T rows (T <= 8) x 64 quads (512 B of each row).  Tile t covers
+// rows  b_low + (k << lo) + (b_high << (lo+T)),  k in [0, 2^T),
+// b_low = t mod 2^lo, b_high = t >> lo, i.e. lo = 0 gives contiguous tiles
+// and lo > 0 gives strided tiles over bits [lo, lo+T) of the row index.
+// ---------------------------------------------------------------------------
+enum Prog : int {
+    GEN_FFT = 0,   // plain load -> FFT layers -> plain store
+    GEN_IFFT,      // plain load -> IFFT layers -> plain store
+    ENC_FIRST,     // gather originals (rows >= a_count are zero) -> IFFT -> store
+    ENC_MID,       // load -> IFFT (skew_ifft) -> FFT (skew_fft) -> store
+    ENC_LAST,      // load -> FFT -> store rows < out_rows
+    ENC_SINGLE,    // gather -> IFFT -> FFT -> store rows < out_rows
+    DEC_FIRST,     // gather received rows * erasure logs -> IFFT -> store
+    DEC_MID,       // load -> IFFT -> (I + in-tile formal derivative) -> FFT -> store
+    DEC_LAST,      // u + L(z) -> FFT -> reveal lost originals -> store them
+    DEC_SINGLE,    // gather*e -> IFFT -> formal derivative -> FFT -> reveal -> store
+    NUM_PROGS
+};
+
+struct PassArgs {
+    uint8_t* out;              // plain store base (row 0 of the transform)
+    const uint8_t* in;         // plain load base (DEC_LAST: z)
+    const uint8_t* in2;        // DEC_LAST: u
+    const uint8_t* seg_a;      // gather source for rows [0, a_count)
+    const uint8_t* seg_b;      // gather source for rows [chunk, chunk + b_count)
+    const uint8_t* flags_a;    // received flags of segment A (nullptr: all present)
+    const uint8_t* flags_b;    // received flags of segment B
+    uint8_t* rest;             // restored-originals output (row 0 = original 0)
+    const uint32_t* elog;      // erasure logs by row (eval_poly output)
+    const uint32_t* skew_entry;
+    const uint32_t* mul_tab;
+    uint64_t S;                // shard bytes
+    uint32_t qrow;             // quads per row = S / 8
+    uint32_t nslab;            // ceil(qrow / 64)
+    uint32_t lo;               // tile bit offset
+    uint32_t a_count, chunk, b_count;
+    uint32_t skew_ifft, skew_fft;
+    uint32_t out_rows;         // ENC_LAST / ENC_SINGLE
+    uint32_t rest_seg_b;       // originals are segment B (high rate) or A (low rate)
+    uint32_t tile_base;        // first tile index of this launch
+};
+
+// Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.
+hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, hipStream_t s);
+
+// Elementwise / small kernels.
+hipError_t launch_mul(uint8_t* x, size_t bytes, uint32_t entry, const uint32_t* mul_tab, hipStream_t s);
+hipError_t launch_xor(uint8_t* x, const uint8_t* y, size_t bytes, hipStream_t s);
+hipError_t launch_formal_derivative(uint8_t* out, const uint8_t* in, size_t shard_count, size_t S, hipStream_t s);
+
+// FWHT / eval_poly.  `work` is a u32[65536] scratch.
+struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.rs decode
+    const uint8_t* flags_a;    // received flags of segment A
+    const uint8_t* flags_b;    // received flags of segment B
+    uint32_t a_count, chunk, b_count;
+    uint32_t pad_fill;         // value of rows [a_count, chunk)   (1 for high rate)
+    uint32_t tail_fill;        // value of rows >= chunk + b_count (1 for low rate)
+};
+hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
+                                       const uint16_t* log_walsh, hipStream_t s);
+hipError_t launch_eval_poly_u16(uint16_t* data, uint32_t* work, const uint16_t* log_walsh, hipStream_t s);
+hipError_t launch_fwht_u16(uint16_t* data, uint32_t* work, hipStream_t s);
+
+}  // namespace rs16

@@ -1,0 +1,537 @@
+"""rs16 -- Python mirror of the reed_solomon_16 API over the MI355X C ABI.
+
+Reference API (malaire/reed-solomon-16 v0.1.0) -> here:
+  reed_solomon_16::encode / decode        (src/lib.rs:242-344)    -> encode(), decode()
+  ReedSolomonEncoder / ReedSolomonDecoder (src/reed_solomon.rs)   -> same names
+  EncoderResult / DecoderResult + Drop    (src/{encoder,decoder}_result.rs)
+  rate::{Default,High,Low}Rate{Encoder,Decoder} (src/rate/*.rs)  -> RateEncoder/RateDecoder(rate=...)
+  Error (src/lib.rs:31-222)                                       -> Error
+  engine::Engine ops (src/engine.rs:140-260) on device arrays     -> Engine methods
+plus the device-resident one-shot path (encode_device / decode_device).
+
+Every call runs through reed-solomon-16_amd/build/librs16.so (HIP, gfx950).
+There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Iterator, Optional, Tuple
+
+import numpy as np
+
+from ._lib import RS16Error, lib
+
+__all__ = [
+    "Error", "Engine", "default_engine", "ReedSolomonEncoder", "ReedSolomonDecoder", "RateEncoder",
+    "RateDecoder", "EncoderResult", "DecoderResult", "encode", "decode", "encode_device", "decode_device",
+    "supports", "validate", "use_high_rate", "encoder_work_count", "decoder_work_count",
+    "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS",
+]
+
+GF_ORDER = 65536
+GF_MODULUS = 65535
+RATE_DEFAULT, RATE_HIGH, RATE_LOW = 0, 1, 2
+_RATES = {"default": 0, "high": 1, "low": 2, 0: 0, 1: 1, 2: 2}
+
+# Error variants in the order of src/lib.rs:31-125 and their payload fields.
+_VARIANTS = {
+    1: ("DifferentShardSize", ("shard_bytes", "got")),
+    2: ("DuplicateOriginalShardIndex", ("index",)),
+    3: ("DuplicateRecoveryShardIndex", ("index",)),
+    4: ("InvalidOriginalShardIndex", ("original_count", "index")),
+    5: ("InvalidRecoveryShardIndex", ("recovery_count", "index")),
+    6: ("InvalidShardSize", ("shard_bytes",)),
+    7: ("NotEnoughShards", ("original_count", "original_received_count", "recovery_received_count")),
+    8: ("TooFewOriginalShards", ("original_count", "original_received_count")),
+    9: ("TooManyOriginalShards", ("original_count",)),
+    10: ("UnsupportedShardCount", ("original_count", "recovery_count")),
+    100: ("DeviceError", ("hip_error",)),
+    101: ("InvalidArgument", ()),
+}
+_CODES = {name: code for code, (name, _) in _VARIANTS.items()}
+
+
+class Error(Exception):
+    """reed_solomon_16::Error.  ``Error("UnsupportedShardCount", original_count=0,
+    recovery_count=1)`` compares equal to the error the library returns."""
+
+    def __init__(self, kind: str, **fields):
+        if kind not in _CODES:
+            raise ValueError(kind)
+        self.kind, self.fields = kind, fields
+        self.code = _CODES[kind]
+        super().__init__(self._message())
+
+    @classmethod
+    def _from_c(cls, e: RS16Error) -> "Error":
+        name, fnames = _VARIANTS.get(e.code, ("InvalidArgument", ()))
+        vals = (e.v0, e.v1, e.v2)
+        err = cls(name, **{f: int(v) for f, v in zip(fnames, vals)})
+        return err
+
+    def _message(self) -> str:
+        e = RS16Error(self.code, 0, 0, 0)
+        vals = list(self.fields.values()) + [0, 0, 0]
+        e.v0, e.v1, e.v2 = vals[0], vals[1], vals[2]
+        buf = C.create_string_buffer(256)
+        lib().rs16_error_message(C.byref(e), buf, 256)
+        return buf.value.decode()
+
+    def __eq__(self, other):
+        return isinstance(other, Error) and (self.kind, self.fields) == (other.kind, other.fields)
+
+    def __hash__(self):
+        return hash((self.kind, tuple(sorted(self.fields.items()))))
+
+    def __repr__(self):
+        return f"Error.{self.kind}({', '.join(f'{k}={v}' for k, v in self.fields.items())})"
+
+
+def _check(rc: int, err: RS16Error):
+    if rc != 0:
+        raise Error._from_c(err)
+
+
+# ---------------------------------------------------------------------------
+# Shard buffers: host (bytes / bytearray / memoryview / numpy) or device
+# (any object with .is_cuda/.data_ptr(), e.g. a torch tensor on ROCm).
+# ---------------------------------------------------------------------------
+def _is_device(x) -> bool:
+    return bool(getattr(x, "is_cuda", False))
+
+
+def _device_ptr_len(x) -> Tuple[int, int]:
+    if not x.is_contiguous():
+        raise ValueError("device shard must be contiguous")
+    return x.data_ptr(), x.numel() * x.element_size()
+
+
+def _host_buf(x):
+    """Returns (ctypes pointer, length, keepalive)."""
+    if isinstance(x, np.ndarray):
+        a = np.ascontiguousarray(x).view(np.uint8).reshape(-1)
+        return a.ctypes.data_as(C.c_void_p), a.size, a
+    if isinstance(x, str):
+        x = x.encode()
+    mv = memoryview(x).cast("B")
+    n = mv.nbytes
+    if n == 0:
+        return None, 0, None
+    if mv.readonly:
+        buf = (C.c_char * n).from_buffer_copy(mv)
+    else:
+        buf = (C.c_char * n).from_buffer(mv)
+    return C.cast(buf, C.c_void_p), n, buf
+
+
+def _shard_len(x) -> int:
+    if _is_device(x):
+        return _device_ptr_len(x)[1]
+    if isinstance(x, np.ndarray):
+        return x.nbytes
+    return memoryview(x.encode() if isinstance(x, str) else x).nbytes
+
+
+# ---------------------------------------------------------------------------
+# Engine
+# ---------------------------------------------------------------------------
+class Engine:
+    """The MI355X engine: GF tables resident in HBM of ``device`` (NoSimd::new
+    analogue, src/engine/engine_nosimd.rs:27-35) plus the Engine trait ops on
+    device shard arrays (src/engine.rs:140-260).  Device arrays are passed as
+    raw device pointers (int) or torch tensors."""
+
+    def __init__(self, device: int = 0):
+        self._err = RS16Error()
+        self.h = lib().rs16_engine_new(device, C.byref(self._err))
+        if not self.h:
+            raise Error._from_c(self._err)
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rs16_engine_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return lib().rs16_engine_stream(self.h) or 0
+
+    def synchronize(self, stream=None):
+        _check(lib().rs16_engine_synchronize(self.h, stream, C.byref(self._err)), self._err)
+
+    # per-pass hipEvent timing (include/rs16.h "Diagnostics")
+    def set_profiling(self, enable: bool):
+        _check(lib().rs16_engine_set_profiling(self.h, int(enable), C.byref(self._err)), self._err)
+
+    def profile_reset(self):
+        lib().rs16_engine_profile_reset(self.h)
+
+    def profile(self) -> dict:
+        """{program name: (total_ms, launches)} since the last reset."""
+        out = {}
+        for p in range(lib().rs16_prog_count()):
+            ms, n = C.c_double(), C.c_uint64()
+            _check(lib().rs16_engine_profile_read(self.h, p, C.byref(ms), C.byref(n), C.byref(self._err)), self._err)
+            if n.value:
+                out[lib().rs16_prog_name(p).decode()] = (ms.value, n.value)
+        return out
+
+    @staticmethod
+    def _ptr(x) -> int:
+        return x.data_ptr() if hasattr(x, "data_ptr") else int(x)
+
+    # Engine trait (device arrays; see include/rs16.h)
+    def fft(self, data, shard_count, shard_bytes, pos, size, truncated_size, skew_delta, stream=None):
+        _check(lib().rs16_engine_fft(self.h, self._ptr(data), shard_count, shard_bytes, pos, size, truncated_size,
+                                     skew_delta, stream, C.byref(self._err)), self._err)
+
+    def ifft(self, data, shard_count, shard_bytes, pos, size, truncated_size, skew_delta, stream=None):
+        _check(lib().rs16_engine_ifft(self.h, self._ptr(data), shard_count, shard_bytes, pos, size, truncated_size,
+                                      skew_delta, stream, C.byref(self._err)), self._err)
+
+    def fft_skew_end(self, data, shard_count, shard_bytes, pos, size, truncated_size, stream=None):
+        _check(lib().rs16_engine_fft_skew_end(self.h, self._ptr(data), shard_count, shard_bytes, pos, size,
+                                              truncated_size, stream, C.byref(self._err)), self._err)
+
+    def ifft_skew_end(self, data, shard_count, shard_bytes, pos, size, truncated_size, stream=None):
+        _check(lib().rs16_engine_ifft_skew_end(self.h, self._ptr(data), shard_count, shard_bytes, pos, size,
+                                               truncated_size, stream, C.byref(self._err)), self._err)
+
+    def fwht(self, data_u16, truncated_size, stream=None):
+        _check(lib().rs16_engine_fwht(self.h, self._ptr(data_u16), truncated_size, stream, C.byref(self._err)),
+               self._err)
+
+    def eval_poly(self, erasures_u16, truncated_size, stream=None):
+        _check(lib().rs16_engine_eval_poly(self.h, self._ptr(erasures_u16), truncated_size, stream,
+                                           C.byref(self._err)), self._err)
+
+    def mul(self, x, nbytes, log_m, stream=None):
+        _check(lib().rs16_engine_mul(self.h, self._ptr(x), nbytes, log_m, stream, C.byref(self._err)), self._err)
+
+    def xor(self, x, y, nbytes, stream=None):
+        _check(lib().rs16_engine_xor(self.h, self._ptr(x), self._ptr(y), nbytes, stream, C.byref(self._err)),
+               self._err)
+
+    def xor_within(self, data, shard_count, shard_bytes, x, y, count, stream=None):
+        _check(lib().rs16_engine_xor_within(self.h, self._ptr(data), shard_count, shard_bytes, x, y, count, stream,
+                                            C.byref(self._err)), self._err)
+
+    def formal_derivative(self, data, shard_count, shard_bytes, stream=None):
+        _check(lib().rs16_engine_formal_derivative(self.h, self._ptr(data), shard_count, shard_bytes, stream,
+                                                   C.byref(self._err)), self._err)
+
+
+_default_engines = {}
+
+
+def default_engine(device: Optional[int] = None) -> Engine:
+    if device is None:
+        device = 0
+    if device not in _default_engines:
+        _default_engines[device] = Engine(device)
+    return _default_engines[device]
+
+
+# ---------------------------------------------------------------------------
+# Rate helpers
+# ---------------------------------------------------------------------------
+def supports(original_count, recovery_count, rate="default") -> bool:
+    if not (0 <= original_count < 2**64 and 0 <= recovery_count < 2**64):
+        return False
+    return bool(lib().rs16_supports(_RATES[rate], original_count, recovery_count))
+
+
+def validate(original_count, recovery_count, shard_bytes, rate="default"):
+    err = RS16Error()
+    _check(lib().rs16_validate(_RATES[rate], original_count, recovery_count, shard_bytes, C.byref(err)), err)
+
+
+def use_high_rate(original_count, recovery_count) -> bool:
+    err = RS16Error()
+    r = lib().rs16_use_high_rate(original_count, recovery_count, C.byref(err))
+    if r < 0:
+        raise Error._from_c(err)
+    return bool(r)
+
+
+def encoder_work_count(high: bool, original_count, recovery_count) -> int:
+    return lib().rs16_encoder_work_count(int(high), original_count, recovery_count)
+
+
+def decoder_work_count(high: bool, original_count, recovery_count) -> int:
+    return lib().rs16_decoder_work_count(int(high), original_count, recovery_count)
+
+
+# ---------------------------------------------------------------------------
+# Results
+# ---------------------------------------------------------------------------
+class EncoderResult:
+    """EncoderResult (src/encoder_result.rs).  Dropping it (``del``, ``with``,
+    or ``drop()``) resets the encoder for a new round, like Drop."""
+
+    def __init__(self, enc: "RateEncoder"):
+        self._enc = enc
+
+    def recovery(self, index: int) -> Optional[bytes]:
+        e = self._enc
+        buf = C.create_string_buffer(e.shard_bytes)
+        r = lib().rs16_encoder_recovery_copy(e.h, index, buf, e.shard_bytes, C.byref(e._err))
+        if r < 0:
+            raise Error._from_c(e._err)
+        return buf.raw if r == 1 else None
+
+    def recovery_device(self, index: int) -> Optional[int]:
+        return lib().rs16_encoder_recovery_device(self._enc.h, index)
+
+    def recovery_iter(self) -> Iterator[bytes]:
+        i = 0
+        while True:
+            r = self.recovery(i)
+            if r is None:
+                return
+            yield r
+            i += 1
+
+    def drop(self):
+        enc, self._enc = self._enc, None
+        if enc is not None and enc.h:
+            lib().rs16_encoder_result_drop(enc.h)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.drop()
+
+    def __del__(self):
+        try:
+            self.drop()
+        except Exception:
+            pass
+
+
+class DecoderResult:
+    """DecoderResult (src/decoder_result.rs)."""
+
+    def __init__(self, dec: "RateDecoder"):
+        self._dec = dec
+
+    def restored_original(self, index: int) -> Optional[bytes]:
+        d = self._dec
+        buf = C.create_string_buffer(d.shard_bytes)
+        r = lib().rs16_decoder_restored_original_copy(d.h, index, buf, d.shard_bytes, C.byref(d._err))
+        if r < 0:
+            raise Error._from_c(d._err)
+        return buf.raw if r == 1 else None
+
+    def restored_original_device(self, index: int) -> Optional[int]:
+        return lib().rs16_decoder_restored_original_device(self._dec.h, index)
+
+    def restored_original_iter(self) -> Iterator[Tuple[int, bytes]]:
+        for i in range(self._dec.original_count):
+            r = self.restored_original(i)
+            if r is not None:
+                yield i, r
+
+    def drop(self):
+        dec, self._dec = self._dec, None
+        if dec is not None and dec.h:
+            lib().rs16_decoder_result_drop(dec.h)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.drop()
+
+    def __del__(self):
+        try:
+            self.drop()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------
+# Encoders / decoders
+# ---------------------------------------------------------------------------
+class RateEncoder:
+    """RateEncoder<E = MI355X engine> (src/rate.rs:113-173) for rate
+    "default" (DefaultRateEncoder), "high" or "low"."""
+
+    def __init__(self, original_count, recovery_count, shard_bytes, rate="default", engine: Optional[Engine] = None):
+        self.engine = engine or default_engine()
+        self._err = RS16Error()
+        self.h = lib().rs16_encoder_new(self.engine.h, _RATES[rate], original_count, recovery_count, shard_bytes,
+                                        C.byref(self._err))
+        if not self.h:
+            raise Error._from_c(self._err)
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rs16_encoder_free(self.h)
+            self.h = None
+
+    @staticmethod
+    def supports(original_count, recovery_count) -> bool:
+        return supports(original_count, recovery_count)
+
+    @property
+    def is_high_rate(self) -> bool:
+        return bool(lib().rs16_encoder_is_high_rate(self.h))
+
+    def reset(self, original_count, recovery_count, shard_bytes):
+        _check(lib().rs16_encoder_reset(self.h, original_count, recovery_count, shard_bytes, C.byref(self._err)),
+               self._err)
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    def add_original_shard(self, shard):
+        if _is_device(shard):
+            p, n = _device_ptr_len(shard)
+            rc = lib().rs16_encoder_add_original_shard_device(self.h, p, n, C.byref(self._err))
+        else:
+            p, n, keep = _host_buf(shard)
+            rc = lib().rs16_encoder_add_original_shard(self.h, p, n, C.byref(self._err))
+        _check(rc, self._err)
+
+    def encode(self) -> EncoderResult:
+        _check(lib().rs16_encoder_encode(self.h, C.byref(self._err)), self._err)
+        return EncoderResult(self)
+
+
+class RateDecoder:
+    """RateDecoder<E = MI355X engine> (src/rate.rs:179-250)."""
+
+    def __init__(self, original_count, recovery_count, shard_bytes, rate="default", engine: Optional[Engine] = None):
+        self.engine = engine or default_engine()
+        self._err = RS16Error()
+        self.h = lib().rs16_decoder_new(self.engine.h, _RATES[rate], original_count, recovery_count, shard_bytes,
+                                        C.byref(self._err))
+        if not self.h:
+            raise Error._from_c(self._err)
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rs16_decoder_free(self.h)
+            self.h = None
+
+    @staticmethod
+    def supports(original_count, recovery_count) -> bool:
+        return supports(original_count, recovery_count)
+
+    @property
+    def is_high_rate(self) -> bool:
+        return bool(lib().rs16_decoder_is_high_rate(self.h))
+
+    def reset(self, original_count, recovery_count, shard_bytes):
+        _check(lib().rs16_decoder_reset(self.h, original_count, recovery_count, shard_bytes, C.byref(self._err)),
+               self._err)
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    def _add(self, original: bool, index, shard):
+        if _is_device(shard):
+            p, n = _device_ptr_len(shard)
+            f = lib().rs16_decoder_add_original_shard_device if original else lib().rs16_decoder_add_recovery_shard_device
+            rc = f(self.h, index, p, n, C.byref(self._err))
+        else:
+            p, n, keep = _host_buf(shard)
+            f = lib().rs16_decoder_add_original_shard if original else lib().rs16_decoder_add_recovery_shard
+            rc = f(self.h, index, p, n, C.byref(self._err))
+        _check(rc, self._err)
+
+    def add_original_shard(self, index, shard):
+        self._add(True, index, shard)
+
+    def add_recovery_shard(self, index, shard):
+        self._add(False, index, shard)
+
+    def decode(self) -> DecoderResult:
+        _check(lib().rs16_decoder_decode(self.h, C.byref(self._err)), self._err)
+        return DecoderResult(self)
+
+
+class ReedSolomonEncoder(RateEncoder):
+    """ReedSolomonEncoder (src/reed_solomon.rs:13-85): DefaultRate + MI355X engine."""
+
+    def __init__(self, original_count, recovery_count, shard_bytes, engine: Optional[Engine] = None):
+        super().__init__(original_count, recovery_count, shard_bytes, "default", engine)
+
+
+class ReedSolomonDecoder(RateDecoder):
+    """ReedSolomonDecoder (src/reed_solomon.rs:93-183)."""
+
+    def __init__(self, original_count, recovery_count, shard_bytes, engine: Optional[Engine] = None):
+        super().__init__(original_count, recovery_count, shard_bytes, "default", engine)
+
+
+# ---------------------------------------------------------------------------
+# One-shot API (src/lib.rs:242-344)
+# ---------------------------------------------------------------------------
+def encode(original_count: int, recovery_count: int, original: Iterable, engine: Optional[Engine] = None):
+    """reed_solomon_16::encode -> list of recovery shards (bytes)."""
+    if not ReedSolomonEncoder.supports(original_count, recovery_count):
+        raise Error("UnsupportedShardCount", original_count=original_count, recovery_count=recovery_count)
+    it = iter(original)
+    first = next(it, None)
+    if first is None:
+        raise Error("TooFewOriginalShards", original_count=original_count, original_received_count=0)
+    enc = ReedSolomonEncoder(original_count, recovery_count, _shard_len(first), engine)
+    enc.add_original_shard(first)
+    for o in it:
+        enc.add_original_shard(o)
+    with enc.encode() as result:
+        return list(result.recovery_iter())
+
+
+def decode(original_count: int, recovery_count: int, original: Iterable, recovery: Iterable,
+           engine: Optional[Engine] = None):
+    """reed_solomon_16::decode -> {index: restored original shard (bytes)}."""
+    if not ReedSolomonDecoder.supports(original_count, recovery_count):
+        raise Error("UnsupportedShardCount", original_count=original_count, recovery_count=recovery_count)
+    original = iter(original)
+    recovery = iter(recovery)
+    first = next(recovery, None)
+    if first is None:
+        n = sum(1 for _ in original)
+        if n == original_count:
+            return {}
+        raise Error("NotEnoughShards", original_count=original_count, original_received_count=n,
+                    recovery_received_count=0)
+    dec = ReedSolomonDecoder(original_count, recovery_count, _shard_len(first[1]), engine)
+    for i, o in original:
+        dec.add_original_shard(i, o)
+    dec.add_recovery_shard(first[0], first[1])
+    for i, r in recovery:
+        dec.add_recovery_shard(i, r)
+    with dec.decode() as result:
+        return dict(result.restored_original_iter())
+
+
+# ---------------------------------------------------------------------------
+# Device-resident one-shot path (the metric path; include/rs16.h)
+# ---------------------------------------------------------------------------
+def encode_device(original_count, recovery_count, shard_bytes, d_original, d_recovery, stream=None,
+                  engine: Optional[Engine] = None):
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_encode_device(eng.h, original_count, recovery_count, shard_bytes, Engine._ptr(d_original),
+                                    Engine._ptr(d_recovery), stream, C.byref(err)), err)
+
+
+def decode_device(original_count, recovery_count, shard_bytes, d_original, d_original_received, d_recovery,
+                  d_recovery_received, original_received_count, recovery_received_count, stream=None,
+                  engine: Optional[Engine] = None):
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_decode_device(eng.h, original_count, recovery_count, shard_bytes, Engine._ptr(d_original),
+                                    Engine._ptr(d_original_received), Engine._ptr(d_recovery),
+                                    Engine._ptr(d_recovery_received), original_received_count,
+                                    recovery_received_count, stream, C.byref(err)), err)
