@@ -1,0 +1,163 @@
+// rs16_misc.hip -- elementwise engine ops (mul, xor, formal derivative) and the
+// FWHT / eval_poly kernels of the MI355X GF(2^16) Reed-Solomon engine.
+#include <algorithm>
+
+#include "rs16_internal.hpp"
+
+namespace rs16 {
+
+typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+typedef const __attribute__((address_space(4))) uint8_t* cu8p;
+
+// ---------------------------------------------------------------------------
+// Elementwise engine ops.
+// ---------------------------------------------------------------------------
+// Engine::mul: x[] *= log_m (NoSimd::mul, src/engine/engine_nosimd.rs:65-79).
+__global__ void __launch_bounds__(256) mul_kernel(uint8_t* x, size_t nquads, uint32_t entry, const uint32_t* mul_tab) {
+    cu32p t = (cu32p)mul_tab + (size_t)entry * TAB_DWORDS;
+    uint32_t tt[20];
+#pragma unroll
+    for (int i = 0; i < 20; i++) tt[i] = t[i];
+    for (size_t q = blockIdx.x * (size_t)blockDim.x + threadIdx.x; q < nquads; q += (size_t)gridDim.x * blockDim.x) {
+        const size_t off = (q >> 3) * 64 + (q & 7) * 4;
+        uint32_t yl = *(uint32_t*)(x + off), yh = *(uint32_t*)(x + off + 32);
+        uint32_t ol = 0, oh = 0;
+        mul_xor(ol, oh, yl, yh, tt);
+        *(uint32_t*)(x + off) = ol;
+        *(uint32_t*)(x + off + 32) = oh;
+    }
+}
+hipError_t launch_mul(uint8_t* x, size_t bytes, uint32_t entry, const uint32_t* mul_tab, hipStream_t s) {
+    const size_t nq = bytes / 8;
+    if (!nq) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>((nq + 255) / 256, 4096);
+    hipLaunchKernelGGL(mul_kernel, dim3(grid), dim3(256), 0, s, x, nq, entry, mul_tab);
+    return hipGetLastError();
+}
+
+// Engine::xor: x[] ^= y[] (src/engine/engine_nosimd.rs:81-88), 16 B per lane.
+__global__ void __launch_bounds__(256) xor_kernel(uint4* x, const uint4* y, size_t n16) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        uint4 a = x[i], b = y[i];
+        x[i] = make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+    }
+}
+hipError_t launch_xor(uint8_t* x, const uint8_t* y, size_t bytes, hipStream_t s) {
+    const size_t n16 = bytes / 16;
+    if (!n16) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>((n16 + 255) / 256, 8192);
+    hipLaunchKernelGGL(xor_kernel, dim3(grid), dim3(256), 0, s, (uint4*)x, (const uint4*)y, n16);
+    return hipGetLastError();
+}
+
+// Engine::formal_derivative (src/engine.rs:233-238), closed form, out of place:
+// out[j] = in[j] ^ XOR_{b : j_b = 0, 2^b < n} in[j | 2^b]   (n a power of two).
+__global__ void __launch_bounds__(256) fd_kernel(uint4* out, const uint4* in, uint32_t n, size_t row16) {
+    const size_t total = (size_t)n * row16;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t j = (uint32_t)(i / row16);
+        const size_t col = i - (size_t)j * row16;
+        uint4 acc = in[i];
+        for (uint32_t b = 1; b < n; b <<= 1)
+            if (!(j & b)) {
+                uint4 v = in[(size_t)(j | b) * row16 + col];
+                acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+            }
+        out[i] = acc;
+    }
+}
+hipError_t launch_formal_derivative(uint8_t* out, const uint8_t* in, size_t n, size_t S, hipStream_t s) {
+    const size_t row16 = S / 16, total = n * row16;
+    if (!total) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(fd_kernel, dim3(grid), dim3(256), 0, s, (uint4*)out, (const uint4*)in, (uint32_t)n, row16);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// FWHT over Z/65535 (reference Engine::fwht, NoSimd::fwht_private
+// src/engine/engine_nosimd.rs:121-183) and eval_poly (src/engine.rs:207-218).
+// The 65536-point transform is two passes of 256-point transforms (row bits
+// 8-15 strided, then bits 0-7 contiguous).  The butterflies are exact ring
+// operations in Z/65535, so layer order does not change any residue; a value
+// may come out as 65535 where the reference has 0 (same residue), which every
+// consumer treats identically (mul by log 0 == mul by log 65535 == x1).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fwht256_lds(uint32_t* s) {
+    const int t = threadIdx.x;  // 256 threads
+#pragma unroll
+    for (int d = 1; d < 256; d <<= 1) {
+        __syncthreads();
+        if (t < 128) {
+            const int i = (t / d) * 2 * d + (t % d), j = i + d;
+            const uint32_t x = s[i], y = s[j];
+            s[i] = add_mod(x, y);
+            s[j] = sub_mod(x, y);
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t erasure_at(const ErasureSpec& e, uint32_t i) {
+    if (i < e.a_count) return e.flags_a ? (((cu8p)e.flags_a)[i] ? 0u : 1u) : 0u;
+    if (i < e.chunk) return e.pad_fill;
+    if (i - e.chunk < e.b_count) return e.flags_b ? (((cu8p)e.flags_b)[i - e.chunk] ? 0u : 1u) : 0u;
+    return e.tail_fill;
+}
+
+// MODE 0: in = u32 work; MODE 1: build erasures from flags; MODE 2: in = u16 data.
+// OUT 0: u32 work/out; OUT 1: u16 data.
+template <int MODE, int OUT>
+__global__ void __launch_bounds__(256) fwht_hi_kernel(ErasureSpec e, const uint32_t* in32, const uint16_t* in16,
+                                                       uint32_t* out32, uint16_t* out16) {
+    __shared__ uint32_t s[256];
+    const uint32_t idx = blockIdx.x + 256u * threadIdx.x;  // bits 8-15 vary within the block
+    uint32_t v;
+    if (MODE == 0) v = in32[idx];
+    else if (MODE == 1) v = erasure_at(e, idx);
+    else v = in16[idx];
+    s[threadIdx.x] = v;
+    fwht256_lds(s);
+    if (OUT == 0) out32[idx] = s[threadIdx.x];
+    else out16[idx] = (uint16_t)s[threadIdx.x];
+}
+
+// Contiguous 256-point FWHT; if MULW, then multiply by log_walsh mod 65535 and
+// do the contiguous FWHT again (the middle of eval_poly).
+template <bool MULW, int IN16, int OUT16>
+__global__ void __launch_bounds__(256) fwht_lo_kernel(const uint32_t* in32, const uint16_t* in16, uint32_t* out32,
+                                                       uint16_t* out16, const uint16_t* log_walsh) {
+    __shared__ uint32_t s[256];
+    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+    s[threadIdx.x] = IN16 ? in16[idx] : in32[idx];
+    fwht256_lds(s);
+    if (MULW) {
+        s[threadIdx.x] = (uint32_t)(((uint64_t)s[threadIdx.x] * log_walsh[idx]) % GF_MODULUS);
+        fwht256_lds(s);
+    }
+    if (OUT16) out16[idx] = (uint16_t)s[threadIdx.x];
+    else out32[idx] = s[threadIdx.x];
+}
+
+hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
+                                       const uint16_t* log_walsh, hipStream_t s) {
+    hipLaunchKernelGGL((fwht_hi_kernel<1, 0>), dim3(256), dim3(256), 0, s, e, nullptr, nullptr, work, nullptr);
+    hipLaunchKernelGGL((fwht_lo_kernel<true, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, work, nullptr, log_walsh);
+    hipLaunchKernelGGL((fwht_hi_kernel<0, 0>), dim3(256), dim3(256), 0, s, e, work, nullptr, out_elog, nullptr);
+    return hipGetLastError();
+}
+hipError_t launch_eval_poly_u16(uint16_t* data, uint32_t* work, const uint16_t* log_walsh, hipStream_t s) {
+    ErasureSpec e{};
+    hipLaunchKernelGGL((fwht_hi_kernel<2, 0>), dim3(256), dim3(256), 0, s, e, nullptr, data, work, nullptr);
+    hipLaunchKernelGGL((fwht_lo_kernel<true, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, work, nullptr, log_walsh);
+    hipLaunchKernelGGL((fwht_hi_kernel<0, 1>), dim3(256), dim3(256), 0, s, e, work, nullptr, nullptr, data);
+    return hipGetLastError();
+}
+hipError_t launch_fwht_u16(uint16_t* data, uint32_t* work, hipStream_t s) {
+    ErasureSpec e{};
+    hipLaunchKernelGGL((fwht_hi_kernel<2, 0>), dim3(256), dim3(256), 0, s, e, nullptr, data, work, nullptr);
+    hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 1>), dim3(256), dim3(256), 0, s, work, nullptr, nullptr, data, nullptr);
+    return hipGetLastError();
+}
+
+}  // namespace rs16

@@ -1,0 +1,20 @@
+"""Summarize rocprofv3 --pmc counter_collection CSVs: per kernel, mean of each
+counter over dispatches (counters summed over XCD/SE instances per dispatch)."""
+import csv, sys, glob, collections, re
+def short(n):
+    m = re.search(r"pass_kernel<(\d+), (\d+)>", n)
+    progs = ["GEN_FFT","GEN_IFFT","ENC_FIRST","ENC_MID","ENC_LAST","ENC_SINGLE","DEC_FIRST","DEC_MID","DEC_LAST","DEC_SINGLE"]
+    if m: return f"{progs[int(m.group(1))]}/T{m.group(2)}"
+    return n.split("(")[0].replace("void rs16::","")[:28]
+acc = collections.defaultdict(lambda: collections.defaultdict(float))
+cnt = collections.defaultdict(lambda: collections.defaultdict(set))
+dur = collections.defaultdict(list)
+for f in sys.argv[1:]:
+    for r in csv.DictReader(open(f)):
+        k = short(r["Kernel_Name"]); c = r["Counter_Name"]
+        acc[k][c] += float(r["Counter_Value"]); cnt[k][c].add(r["Dispatch_Id"])
+        dur[k].append((r["Dispatch_Id"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+for k in acc:
+    d = dict(dur[k]); us = sum(d.values()) / len(d) / 1e3
+    vals = {c: acc[k][c] / len(cnt[k][c]) for c in acc[k]}
+    print(f"{k:16s} {us:8.1f}us " + " ".join(f"{c}={v:.4g}" for c, v in sorted(vals.items())))
