@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1000:1000 side measurements")
+    p.add_argument("--no-verify", action="store_true", help="diagnostic (ablation) builds only")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     return p.parse_args()
 
@@ -188,10 +189,12 @@ def main():
         want = {(c["k"], c["m"]): c["recovery_sha256"] for c in fx["cases"]}.get((k, m))
         if want is not None:
             got = hashlib.sha256(recovery.tobytes()).hexdigest()
-            assert got == want, f"recovery hash {got} != oracle fixture {want}"
+            assert args.no_verify or got == want, f"recovery hash {got} != oracle fixture {want}"
             verified = "recovery SHA-256 == oracle fixture; " + verified
     decode()
-    assert np.array_equal(d_rest.download(shape=(k, S)), original), "decode did not restore the originals"
+    assert args.no_verify or np.array_equal(d_rest.download(shape=(k, S)), original), "decode did not restore"
+    if args.no_verify:
+        verified = "NOT VERIFIED (diagnostic build)"
 
     def barrier():
         eng.synchronize()
