@@ -56,7 +56,6 @@ static PassArgs base_args(const rs16_engine* e, size_t S) {
     a.mul_tab = e->d_mul_tab;
     a.S = S;
     a.qrow = (uint32_t)(S / 8);
-    a.nslab = (a.qrow + 63) / 64;
     return a;
 }
 
@@ -241,14 +240,19 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_
     a.lo = 0;
     a.out = Z;
     RS16_PASS(DEC_FIRST, lo, a, 1u << hi, s);
-    a.lo = lo;
-    a.in = Z;
-    a.out = U;
-    RS16_PASS(DEC_MID, hi, a, 1u << lo, s);
-    // Only tiles that contain original rows are needed in the last pass.
+    // Only tiles that contain original rows are needed in the last pass,
+    // so DEC_MID computes and stores only U rows of those tiles (its tile
+    // row k is row bits [lo, L) = the last pass's tile index).
     const uint32_t ob = g.high ? g.chunk : 0;
     const uint32_t oc = g.high ? g.b_count : g.a_count;
     const uint32_t t0 = ob >> lo, t1 = (uint32_t)(((size_t)ob + oc + ((size_t)1 << lo) - 1) >> lo);
+    a.lo = lo;
+    a.in = Z;
+    a.out = U;
+    a.need_lo = t0;
+    a.need_hi = t1;
+    RS16_PASS(DEC_MID, hi, a, 1u << lo, s);
+    a.need_lo = a.need_hi = 0;
     a.lo = 0;
     a.in = Z;
     a.in2 = U;

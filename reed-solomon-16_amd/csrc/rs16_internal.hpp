@@ -20,7 +20,9 @@ const HostTables& host_tables();
 
 // ---------------------------------------------------------------------------
 // Pass kernels.  A "pass" applies a contiguous range of FFT/IFFT layers to
-// tiles of 2^T rows (T <= 8) x 64 quads (512 B of each row).  Tile t covers
+// tiles of 2^T rows (T <= 8) x Q quads (Q = 32 for T > 4, else 64; a quad is
+// 8 bytes of a row, rs16_gf.hpp), one workgroup per (tile, slab of Q quads).
+// Tile t covers
 // rows  b_low + (k << lo) + (b_high << (lo+T)),  k in [0, 2^T),
 // b_low = t mod 2^lo, b_high = t >> lo, i.e. lo = 0 gives contiguous tiles
 // and lo > 0 gives strided tiles over bits [lo, lo+T) of the row index.
@@ -53,13 +55,17 @@ struct PassArgs {
     const uint32_t* mul_tab;
     uint64_t S;                // shard bytes
     uint32_t qrow;             // quads per row = S / 8
-    uint32_t nslab;            // ceil(qrow / 64)
+    uint32_t nslab;            // ceil(qrow / Q), set by launch_pass
     uint32_t lo;               // tile bit offset
     uint32_t a_count, chunk, b_count;
     uint32_t skew_ifft, skew_fft;
     uint32_t out_rows;         // ENC_LAST / ENC_SINGLE
     uint32_t rest_seg_b;       // originals are segment B (high rate) or A (low rate)
     uint32_t tile_base;        // first tile index of this launch
+    // DEC_MID output pruning: only tile rows k in [need_lo, need_hi) are
+    // consumed downstream; FFT groups and stores outside it are skipped.
+    // need_hi == 0: no pruning.
+    uint32_t need_lo, need_hi;
 };
 
 // Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.

@@ -7,23 +7,26 @@
 // Structure of one pass
 // ---------------------
 //   A transform of 2^L rows runs in ceil(L/8) HBM passes.  A pass loads a
-//   tile of 2^T rows (T <= 8) x 64 quads (512 B of each row; a quad = 4
-//   elements = one lo dword + one hi dword, rs16_gf.hpp), applies T layers
+//   tile of 2^T rows (T <= 8) x Q quads (a quad = 4 elements = one lo dword
+//   + one hi dword, rs16_gf.hpp; Q = 32 for T > 4, else 64), applies T layers
 //   and stores it.  Tile t covers rows  b_low + (k << lo) + (b_high << (lo+T)),
 //   k in [0, 2^T): lo = 0 gives contiguous tiles, lo > 0 strided ones.
 //
-//   Workgroup = 2^(T-4) waves, lane = quad, so every twiddle (a function of
-//   the row index only) is wave-uniform.  Each thread keeps 16 rows of its
-//   quad in VGPRs: the 4 layers whose row bits are in registers are radix-16
-//   butterfly networks with no data movement; one LDS transpose switches
-//   between layout A (k bits 0-3 in registers) and layout B (k bits T-4..T-1).
+//   Lane = quad.  Each thread keeps 16 rows ("a row set") of its quad in
+//   VGPRs; a wave holds 64/Q row sets.  The 4 layers whose row bits are in
+//   registers are radix-16 butterfly networks with no data movement; LDS
+//   transposes switch between layout A (k bits 0-3 in registers) and layout B
+//   (k bits T-4..T-1).  The transpose runs in NQR rounds of QL quads so that
+//   the LDS image is at most 32 KiB and two or three workgroups share a CU:
+//   one workgroup's HBM loads and stores overlap another's butterflies.
 //
 //   Twiddle tables: a tile needs 2^T - 1 distinct twiddles per transform
 //   direction (one per (layer, group)).  Their 80-byte v_perm multiply tables
-//   are staged into LDS once per workgroup and read with broadcast
-//   ds_read_b128 (5 per group), one group ahead of use.  Groups are compiled
-//   as a straight-line sequence separated by register pins, so a wave holds
-//   at most two tables.
+//   are staged into LDS once per workgroup and read with ds_read_b128
+//   (5 per group, broadcast within each row set), one group ahead of use.
+//   Groups are compiled as a straight-line sequence separated by register
+//   pins, so a wave holds at most two tables.  The decoder's per-row erasure
+//   multipliers (gather and reveal) are staged the same way.
 //
 //   Butterflies (bit-exact spec, the reference's):
 //     FFT  layer d: a ^= b * skew[r + d + skew_delta - 1];  b ^= a
@@ -33,9 +36,6 @@
 #include "rs16_internal.hpp"
 
 namespace rs16 {
-
-typedef const __attribute__((address_space(4))) uint32_t* cu32p;
-typedef const __attribute__((address_space(4))) uint8_t* cu8p;
 
 enum LoadMode { LD_PLAIN = 0, LD_GATHER_ENC, LD_GATHER_DEC, LD_DEC_LAST };
 enum StoreMode { ST_PLAIN = 0, ST_RECOVERY, ST_RESTORE };
@@ -63,17 +63,25 @@ RS16_PROG(DEC_SINGLE, LD_GATHER_DEC, true, true, true, ST_RESTORE)
 
 template <int T> struct Geo {
     static constexpr int R = T > 4 ? 4 : T;               // row bits held in registers
-    static constexpr int NR = 1 << R;                     // rows per thread
-    static constexpr int W = T > 4 ? (1 << (T - 4)) : 1;  // waves per workgroup
-    static constexpr int SHB = T - R;                     // layout B: k = w + (m << SHB)
+    static constexpr int NR = 1 << R;                     // rows per thread (a row set)
+    static constexpr int Q = T > 4 ? 32 : 64;             // quads per tile row
+    static constexpr int HWS = 64 / Q;                    // row sets per wave
+    static constexpr int SETS = 1 << (T - R);             // row sets per tile
+    static constexpr int W = SETS / HWS > 0 ? SETS / HWS : 1;  // waves per workgroup
+    static constexpr int SHB = T - R;                     // layout B: k = s + (m << SHB)
     static constexpr int THREADS = 64 * W;
     static constexpr int NTAB = (1 << T) - 1;             // twiddle groups per direction
     // Tables of layers kb >= 4 (layout-B phase) come last: t >= TSPLIT.
     static constexpr int TSPLIT = T > 4 ? (1 << T) - (1 << (T - 4)) : 0;
+    // LDS transposes run in NQR rounds of QL quads (image <= 32 KiB).
+    static constexpr int QL = (4096 >> T) < Q ? (4096 >> T) : Q;
+    static constexpr int NQR = Q / QL;
 };
 
 // Dynamic LDS layout of program P at tile bits T (bytes):
-//   [data tile: 2^T x 64 x 8][tab1: NTAB x 80][tab2: (NTAB - TSPLIT) x 80]
+//   [data image: 2^T x QL x 8][tab1: NTAB x 80][tab2: (NTAB - TSPLIT) x 80]
+//   [ert: 2^T x 80 (gather multipliers)][rvt: 2^T x 80 (reveal multipliers)]
+//   [lost: 2^T x u32 (row is a lost original)]
 // tab1 holds the first direction's tables; in two-direction programs tab2
 // holds the second direction's layout-B tables and its layout-A tables are
 // restaged into tab1 once the first direction's layout-A phase is done.
@@ -81,31 +89,51 @@ template <int P, int T> struct Smem {
     using PT = ProgTraits<P>;
     static constexpr bool TWO = PT::IFFT && PT::FFT;
     static constexpr bool DATA = T > 4 || PT::FD || PT::LOAD == LD_DEC_LAST;
-    static constexpr int DATA_BYTES = DATA ? (1 << T) * 64 * 8 : 0;
+    static constexpr int DATA_BYTES = DATA ? (1 << T) * Geo<T>::QL * 8 : 0;
     static constexpr int TAB1_BYTES = Geo<T>::NTAB * 80;
     static constexpr int TAB2_BYTES = TWO ? (Geo<T>::NTAB - Geo<T>::TSPLIT) * 80 : 0;
-    static constexpr int BYTES = DATA_BYTES + TAB1_BYTES + TAB2_BYTES;
+    static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
+    static constexpr int RVT_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 80 : 0;
+    static constexpr int LOST_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 4 : 0;
+    static constexpr int TAB1_OFF = DATA_BYTES;
+    static constexpr int TAB2_OFF = TAB1_OFF + TAB1_BYTES;
+    static constexpr int ERT_OFF = TAB2_OFF + TAB2_BYTES;
+    static constexpr int RVT_OFF = ERT_OFF + ERT_BYTES;
+    static constexpr int LOST_OFF = RVT_OFF + RVT_BYTES;
+    static constexpr int BYTES = LOST_OFF + LOST_BYTES;
 };
 
 struct Thr {
-    uint32_t lane, w, b_low, b_high, offL;
+    uint32_t lane, w, s;   // lane, wave, row set
+    uint32_t ql, round;    // quad within the LDS round, LDS round
+    uint32_t b_low, b_high, offL;
     bool active;
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 template <int T, bool LB> __device__ __forceinline__ uint32_t kidx(const Thr& c, int m) {
-    return LB ? c.w + ((uint32_t)m << Geo<T>::SHB) : (c.w << Geo<T>::R) + (uint32_t)m;
+    return LB ? c.s + ((uint32_t)m << Geo<T>::SHB) : (c.s << Geo<T>::R) + (uint32_t)m;
 }
 
 template <int T> __device__ __forceinline__ uint32_t row_rel(const Thr& c, const PassArgs& a, uint32_t k) {
     return c.b_low + (k << a.lo) + (c.b_high << (a.lo + T));
 }
 
-__device__ __forceinline__ void ld_quad(const uint8_t* row, const Thr& c, uint32_t& L, uint32_t& H);
-__device__ __forceinline__ void st_quad(uint8_t* row, const Thr& c, uint32_t L, uint32_t H);
+// Diagnostic ablation builds (never the shipped library):
+//   -DRS16_ABLATE=1  compile the butterfly layers out (memory + staging only)
+//   -DRS16_ABLATE=2  compile HBM loads/stores out (compute only)
+//   -DRS16_ABLATE=3  as 1, and no table staging
+//   -DRS16_ABLATE=4  as 1, and no LDS exchanges / formal derivative
+#ifndef RS16_ABLATE
+#define RS16_ABLATE 0
+#endif
+#ifndef RS16_NO_PIN
+#define RS16_NO_PIN 0
+#endif
+
 __device__ __forceinline__ void ld_quad(const uint8_t* row, const Thr& c, uint32_t& L, uint32_t& H) {
-#if defined(RS16_ABLATE) && RS16_ABLATE == 2
+#if RS16_ABLATE == 2
     L = (uint32_t)(uintptr_t)row ^ c.offL;
     H = L * 3u;
     return;
@@ -118,21 +146,13 @@ __device__ __forceinline__ void ld_quad(const uint8_t* row, const Thr& c, uint32
     }
 }
 __device__ __forceinline__ void st_quad(uint8_t* row, const Thr& c, uint32_t L, uint32_t H) {
-#if defined(RS16_ABLATE) && RS16_ABLATE == 2
+#if RS16_ABLATE == 2
     if ((L ^ H) != 0x9e3779b9u) return;  // keeps the results live, (almost) never stores
 #endif
     if (c.active) {
         *(uint32_t*)(row + c.offL) = L;
         *(uint32_t*)(row + c.offL + 32) = H;
     }
-}
-
-// Table of a twiddle from global memory into SGPRs (used for the per-row
-// erasure multiplies, which are few).
-__device__ __forceinline__ void load_table_global(uint32_t (&t)[20], const PassArgs& a, uint32_t e) {
-    cu32p p = (cu32p)a.mul_tab + e * TAB_DWORDS;
-#pragma unroll
-    for (int i = 0; i < 20; i++) t[i] = p[i];
 }
 
 __device__ __forceinline__ void load_table_lds(uint32_t (&t)[20], const uint4* p) {
@@ -147,44 +167,89 @@ __device__ __forceinline__ void load_table_lds(uint32_t (&t)[20], const uint4* p
 }
 
 // ---------------------------------------------------------------------------
-// Twiddle-table staging.  Group id t in [0, 2^T-1): layer kb with
-// offset(kb) = 2^T - 2^(T-kb) <= t < offset(kb+1), group j = t - offset(kb)
-// covering tile rows k with k >> (kb+1) == j.
+// Table staging.  N tables of 5 x 16 B, table i taken from mul_tab entry
+// entry(i), spread over the workgroup's threads.  Split into issue (global
+// loads into registers, issued next to the tile's own loads so that their
+// latencies overlap) and commit (ds_write, before the barrier that
+// publishes the tables).
 // ---------------------------------------------------------------------------
-// Staging is split into issue (global loads into registers, issued next to
-// the tile's own loads so their latencies overlap) and commit (ds_write,
-// before the barrier that publishes the tables).  N = number of groups.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <int T, int N> struct Stager {
     static constexpr int PER = (N * 5 + Geo<T>::THREADS - 1) / Geo<T>::THREADS;
     u32x4 v[PER > 0 ? PER : 1];
-    int di[PER > 0 ? PER : 1];
 
-    __device__ __forceinline__ void issue(int t_begin, int t_base, uint32_t skew, const Thr& c, const PassArgs& a) {
-        const uint32_t* sk = a.skew_entry;
+    template <class F> __device__ __forceinline__ void issue(const PassArgs& a, F entry) {
+        if (RS16_ABLATE == 3) return;
         const u32x4* tab = (const u32x4*)a.mul_tab;
 #pragma unroll
         for (int i = 0; i < PER; i++) {
             const int idx = (int)threadIdx.x + i * Geo<T>::THREADS;
-            di[i] = -1;
-            if (idx < N * 5) {
-                const int t = t_begin + idx / 5, part = idx % 5;
-                int kb = 0;
-                while (t >= (1 << T) - (1 << (T - kb - 1))) kb++;
-                const uint32_t j = (uint32_t)(t - ((1 << T) - (1 << (T - kb))));
-                const uint32_t d = 1u << (a.lo + kb);
-                const uint32_t g = (c.b_high << (a.lo + T)) + (j << (kb + 1 + a.lo));
-                const uint32_t e = sk[g + d + skew - 1];
-                v[i] = tab[(size_t)e * (TAB_DWORDS / 4) + part];
-                di[i] = (t - t_base) * 5 + part;
-            }
+            if (idx < N * 5) v[i] = tab[(size_t)entry(idx / 5) * (TAB_DWORDS / 4) + idx % 5];
         }
     }
     __device__ __forceinline__ void commit(uint4* dst) const {
+        if (RS16_ABLATE == 3) return;
         u32x4* d = (u32x4*)dst;
 #pragma unroll
-        for (int i = 0; i < PER; i++)
-            if (di[i] >= 0) d[di[i]] = v[i];
+        for (int i = 0; i < PER; i++) {
+            const int idx = (int)threadIdx.x + i * Geo<T>::THREADS;
+            if (idx < N * 5) d[idx] = v[i];
+        }
+    }
+};
+
+// Twiddle of tile group t (t in [0, 2^T - 1)): layer kb with
+// offset(kb) = 2^T - 2^(T-kb) <= t < offset(kb+1), group j = t - offset(kb)
+// covering tile rows k with k >> (kb+1) == j.
+template <int T> struct TwiddleEntry {
+    const PassArgs& a;
+    const Thr& c;
+    int t_begin;
+    uint32_t skew;
+    __device__ __forceinline__ uint32_t operator()(int i) const {
+        const int t = t_begin + i;
+        int kb = 0;
+        while (t >= (1 << T) - (1 << (T - kb - 1))) kb++;
+        const uint32_t j = (uint32_t)(t - ((1 << T) - (1 << (T - kb))));
+        const uint32_t d = 1u << (a.lo + kb);
+        const uint32_t g = (c.b_high << (a.lo + T)) + (j << (kb + 1 + a.lo));
+        return a.skew_entry[g + d + skew - 1];
+    }
+};
+
+// Received?  Rows [0, a_count) are segment A, [chunk, chunk + b_count)
+// segment B; anything else is an absent (zero) row.
+__device__ __forceinline__ bool row_received(const PassArgs& a, uint32_t r) {
+    if (r < a.a_count) return !a.flags_a || a.flags_a[r];
+    if (r >= a.chunk && r - a.chunk < a.b_count) return !a.flags_b || a.flags_b[r - a.chunk];
+    return false;
+}
+// Lost original?  (the rows the decoder reveals)
+__device__ __forceinline__ bool row_lost_original(const PassArgs& a, uint32_t r) {
+    const uint32_t base = a.rest_seg_b ? a.chunk : 0;
+    const uint32_t cnt = a.rest_seg_b ? a.b_count : a.a_count;
+    const uint8_t* fl = a.rest_seg_b ? a.flags_b : a.flags_a;
+    return r >= base && r - base < cnt && fl && !fl[r - base];
+}
+
+// "MULTIPLY SHARDS" of rate_high.rs:203-228 / rate_low.rs:203-228: received
+// row r is multiplied by erasure log e[r]; absent rows by zero.
+template <int T> struct GatherEntry {
+    const PassArgs& a;
+    const Thr& c;
+    __device__ __forceinline__ uint32_t operator()(int k) const {
+        const uint32_t r = row_rel<T>(c, a, (uint32_t)k);
+        return row_received(a, r) ? a.elog[r] : ZERO_ENTRY;
+    }
+};
+// REVEAL ERASURES (rate_high.rs:236-242 / rate_low.rs:236-242): lost
+// original row r -> work[r] * (GF_MODULUS - e[r]).
+template <int T> struct RevealEntry {
+    const PassArgs& a;
+    const Thr& c;
+    __device__ __forceinline__ uint32_t operator()(int k) const {
+        const uint32_t r = row_rel<T>(c, a, (uint32_t)k);
+        return row_lost_original(a, r) ? GF_MODULUS - a.elog[r] : ZERO_ENTRY;
     }
 };
 
@@ -213,16 +278,17 @@ template <int T, bool LB, int KB0, int KB1, bool FFT> struct LayerSeq {
 };
 
 // Where group G's table lives: tile group id t = offset(kb) + j, with
-// j = k >> (kb+1) of the group's rows; in two-direction kernels the second
-// direction's layout-B tables are in tab2.
+// j = k >> (kb+1) of the group's rows (per row set in layout A, uniform in
+// layout B); in two-direction kernels the second direction's layout-B
+// tables are in tab2.
 template <int T, bool LB, int KB0, int KB1, bool FFT, int G, bool IN_TAB2>
 __device__ __forceinline__ const uint4* group_table(const Thr& c, const uint4* tab1, const uint4* tab2) {
     using S = LayerSeq<T, LB, KB0, KB1, FFT>;
     constexpr int s = S::step_of(G), gi = S::index_of(G);
     constexpr int kb = S::kb_of(s);
     constexpr int off = (1 << T) - (1 << (T - kb));
-    // layout A: k = (w << R) + m  ->  j = (w << (R-1-kb)) + gi ; layout B: j = gi
-    const uint32_t j = LB ? (uint32_t)gi : (c.w << (Geo<T>::R - 1 - kb)) + gi;
+    // layout A: k = (s << R) + m  ->  j = (s << (R-1-kb)) + gi ; layout B: j = gi
+    const uint32_t j = LB ? (uint32_t)gi : (c.s << (Geo<T>::R - 1 - kb)) + gi;
     const uint32_t t = off + j;
     if (IN_TAB2) return tab2 + (t - Geo<T>::TSPLIT) * 5;
     return tab1 + t * 5;
@@ -242,84 +308,118 @@ template <int NR> __device__ __forceinline__ void pin_rows(uint32_t (&L)[NR], ui
     }
 }
 
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int G> struct GroupLoop {
+// PRUNE (layout-B FFT groups of DEC_MID): a group whose rows
+// [gi << (kb+1), (gi+1) << (kb+1)) miss [need_lo, need_hi) feeds no
+// consumed output and is skipped (the condition is uniform).
+template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, bool PRUNE, int G> struct GroupLoop {
     static __device__ __forceinline__ void run(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
-                                               const uint4* tab1, const uint4* tab2, const uint32_t (&cur)[20]) {
+                                               const PassArgs& a, const uint4* tab1, const uint4* tab2,
+                                               const uint32_t (&cur)[20]) {
         using S = LayerSeq<T, LB, KB0, KB1, FFT>;
         constexpr int s = S::step_of(G), gi = S::index_of(G);
-        constexpr int rb = S::kb_of(s) - S::SH;
+        constexpr int kb = S::kb_of(s);
+        constexpr int rb = kb - S::SH;
         constexpr bool more = G + 1 < S::total();
         uint32_t nxt[20];
         if constexpr (more)
             load_table_lds(nxt, group_table<T, LB, KB0, KB1, FFT, G + 1, IN_TAB2>(c, tab1, tab2));
+        __builtin_amdgcn_sched_barrier(0);  // the prefetch is issued before this group's work
+        bool need = true;
+        if constexpr (PRUNE)
+            need = ((uint32_t)gi << (kb + 1)) < a.need_hi && ((uint32_t)(gi + 1) << (kb + 1)) > a.need_lo;
+        if (need) {
 #pragma unroll
-        for (int j = 0; j < (1 << rb); j++) {
-            const int m = (gi << (rb + 1)) + j, m2 = m + (1 << rb);
-            if (FFT) {
-                mul_xor(L[m], H[m], L[m2], H[m2], cur);
-                L[m2] ^= L[m];
-                H[m2] ^= H[m];
-            } else {
-                L[m2] ^= L[m];
-                H[m2] ^= H[m];
-                mul_xor(L[m], H[m], L[m2], H[m2], cur);
+            for (int j = 0; j < (1 << rb); j++) {
+                const int m = (gi << (rb + 1)) + j, m2 = m + (1 << rb);
+                if (FFT) {
+                    mul_xor(L[m], H[m], L[m2], H[m2], cur);
+                    L[m2] ^= L[m];
+                    H[m2] ^= H[m];
+                } else {
+                    L[m2] ^= L[m];
+                    H[m2] ^= H[m];
+                    mul_xor(L[m], H[m], L[m2], H[m2], cur);
+                }
             }
         }
+#if !RS16_NO_PIN
         pin_rows<Geo<T>::NR>(L, H);
+#endif
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (more) GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, G + 1>::run(L, H, c, tab1, tab2, nxt);
+        if constexpr (more)
+            GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, G + 1>::run(L, H, c, a, tab1, tab2, nxt);
     }
 };
 
 // Apply the layers for k-bits [KB0, KB1) held in registers of layout LB.
-// Diagnostic ablation builds (never the shipped library):
-//   -DRS16_ABLATE=1  compile the butterfly layers out (memory + staging only)
-//   -DRS16_ABLATE=2  compile HBM loads/stores out (compute only)
-#ifndef RS16_ABLATE
-#define RS16_ABLATE 0
-#endif
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2>
+template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, bool PRUNE = false>
 __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
-                                       const uint4* tab1, const uint4* tab2) {
-    if constexpr (KB1 > KB0 && RS16_ABLATE != 1) {
+                                       const PassArgs& a, const uint4* tab1, const uint4* tab2) {
+    if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2)) {
         uint32_t t0[20];
         load_table_lds(t0, group_table<T, LB, KB0, KB1, FFT, 0, IN_TAB2>(c, tab1, tab2));
-        GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, 0>::run(L, H, c, tab1, tab2, t0);
+        GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0>::run(L, H, c, a, tab1, tab2, t0);
     }
 }
 
-template <int T, bool FROM_B>
-__device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
+// LDS image of the data: row k, quad ql of the current round.
+template <int T> __device__ __forceinline__ uint2* img(uint2* lds, const Thr& c, uint32_t k) {
+    return lds + k * Geo<T>::QL + c.ql;
+}
+
+template <int T> __device__ __forceinline__ bool my_round(const Thr& c, int r) {
+    return Geo<T>::NQR == 1 || c.round == (uint32_t)r;
+}
+
+template <int T, bool LB>
+__device__ __forceinline__ void put_rows(const uint32_t (&L)[Geo<T>::NR], const uint32_t (&H)[Geo<T>::NR],
+                                         const Thr& c, uint2* lds) {
+#pragma unroll
+    for (int m = 0; m < Geo<T>::NR; m++) *img<T>(lds, c, kidx<T, LB>(c, m)) = make_uint2(L[m], H[m]);
+}
+template <int T, bool LB>
+__device__ __forceinline__ void get_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                          uint2* lds) {
 #pragma unroll
-    for (int m = 0; m < Geo<T>::NR; m++) lds[kidx<T, FROM_B>(c, m) * 64 + c.lane] = make_uint2(L[m], H[m]);
-    __syncthreads();
-#pragma unroll
     for (int m = 0; m < Geo<T>::NR; m++) {
-        uint2 v = lds[kidx<T, !FROM_B>(c, m) * 64 + c.lane];
+        const uint2 v = *img<T>(lds, c, kidx<T, LB>(c, m));
         L[m] = v.x;
         H[m] = v.y;
     }
-    __syncthreads();
 }
 
-// y[k] ^= XOR_{b < T, k_b = 0} x[k | 2^b] with x read from LDS: the formal
-// derivative restricted to the tile's row bits (Engine::formal_derivative,
+// y[k] ^= XOR_{b < T, k_b = 0} x[k | 2^b] with x read from the LDS image: the
+// formal derivative restricted to the tile's row bits (Engine::formal_derivative,
 // src/engine.rs:233-238, in closed form -- step i = (j & ~(2^b-1)) | 2^b XORs
 // row j|2^b into row j, and that source row is never written before it is read).
+// Row bits held in registers are compile-time: their terms are kept or
+// dropped statically.  Row-set bits differ between lanes: those terms are
+// read unconditionally (for k_b = 1 the address is the row itself) and
+// masked with a select, so all reads of a row issue back to back.
 template <int T, bool LB>
 __device__ __forceinline__ void fd_from_lds(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
-                                            const uint2* lds) {
+                                            uint2* lds) {
+    constexpr int R = Geo<T>::R, SHB = Geo<T>::SHB;
 #pragma unroll
     for (int m = 0; m < Geo<T>::NR; m++) {
         const uint32_t k = kidx<T, LB>(c, m);
         uint32_t xl = L[m], xh = H[m];
 #pragma unroll
         for (int b = 0; b < T; b++) {
-            if (!((k >> b) & 1)) {
-                uint2 v = lds[(k | (1u << b)) * 64 + c.lane];
-                xl ^= v.x;
-                xh ^= v.y;
+            // is bit b of k a register (compile-time) bit?
+            const bool reg_bit = LB ? (b >= SHB) : (b < R);
+            if (reg_bit) {
+                const int mb = LB ? b - SHB : b;
+                if (!((m >> mb) & 1)) {
+                    const uint2 v = *img<T>(lds, c, k | (1u << b));
+                    xl ^= v.x;
+                    xh ^= v.y;
+                }
+            } else {
+                const uint2 v = *img<T>(lds, c, k | (1u << b));
+                const bool take = !((k >> b) & 1);
+                xl ^= take ? v.x : 0u;
+                xh ^= take ? v.y : 0u;
             }
         }
         L[m] = xl;
@@ -327,35 +427,91 @@ __device__ __forceinline__ void fd_from_lds(uint32_t (&L)[Geo<T>::NR], uint32_t 
     }
 }
 
+// Layout switch through LDS, in rounds.  `mid` runs after the first barrier
+// (every wave is past its previous phase, so that phase's tables are dead).
+template <int T, bool FROM_B, class MID>
+__device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
+                                         uint2* lds, MID mid) {
+    if (RS16_ABLATE == 4) return mid();
+#pragma unroll
+    for (int r = 0; r < Geo<T>::NQR; r++) {
+        if (my_round<T>(c, r)) put_rows<T, FROM_B>(L, H, c, lds);
+        __syncthreads();
+        if (r == 0) mid();
+        if (my_round<T>(c, r)) get_rows<T, !FROM_B>(L, H, c, lds);
+        __syncthreads();
+    }
+}
+
+// y = x + (in-tile formal derivative part) of the rows in registers, where
+// the LDS image is filled from (SL, SH) -- the rows themselves for the
+// (I + H) step of DEC_MID, z for DEC_LAST's y = u + L(z).  In rounds.
+template <int T, bool LB>
+__device__ __forceinline__ void tile_fd(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR],
+                                        const uint32_t (&SL)[Geo<T>::NR], const uint32_t (&SH)[Geo<T>::NR],
+                                        const Thr& c, uint2* lds) {
+    if (RS16_ABLATE == 4) return;
+#pragma unroll
+    for (int r = 0; r < Geo<T>::NQR; r++) {
+        if (my_round<T>(c, r)) put_rows<T, LB>(SL, SH, c, lds);
+        __syncthreads();
+        if (my_round<T>(c, r)) fd_from_lds<T, LB>(L, H, c, lds);
+        __syncthreads();
+    }
+}
+
+struct NoMid {
+    __device__ __forceinline__ void operator()() const {}
+};
+
 template <int P, int T>
-__global__ void __launch_bounds__(Geo<T>::THREADS) pass_kernel(PassArgs a) {
+__global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pass_kernel(PassArgs a) {
     using PT = ProgTraits<P>;
     using SM = Smem<P, T>;
-    constexpr int NR = Geo<T>::NR;
-    constexpr int R = Geo<T>::R;
+    using G = Geo<T>;
+    constexpr int NR = G::NR;
+    constexpr int R = G::R;
     constexpr bool TWO = SM::TWO;
+    constexpr bool PRUNE = P == DEC_MID;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint2* lds = (uint2*)smem;
-    uint4* tab1 = (uint4*)(smem + SM::DATA_BYTES);
-    uint4* tab2 = (uint4*)(smem + SM::DATA_BYTES + SM::TAB1_BYTES);
+    uint4* tab1 = (uint4*)(smem + SM::TAB1_OFF);
+    uint4* tab2 = (uint4*)(smem + SM::TAB2_OFF);
+    uint4* ert = (uint4*)(smem + SM::ERT_OFF);
+    uint4* rvt = (uint4*)(smem + SM::RVT_OFF);
+    uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
+
+    // Block -> (tile, slab): when the grid is a multiple of 8, each XCD
+    // (blocks are dealt to the 8 XCDs round-robin) gets a contiguous range
+    // of (tile, slab), so the slabs of a tile share their twiddle tables in
+    // one L2.
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t gid = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
+    const uint32_t slab = gid % a.nslab;
+    const uint32_t tile = gid / a.nslab + a.tile_base;
 
     Thr c;
     c.lane = threadIdx.x & 63;
     c.w = uni(threadIdx.x >> 6);
-    const uint32_t slab = blockIdx.x % a.nslab;
-    const uint32_t tile = blockIdx.x / a.nslab + a.tile_base;
+    const uint32_t qt = c.lane % G::Q;
+    c.s = c.w * G::HWS + c.lane / G::Q;
+    c.ql = qt % G::QL;
+    c.round = qt / G::QL;
     c.b_low = tile & ((1u << a.lo) - 1);
     c.b_high = tile >> a.lo;
-    const uint32_t Q = slab * 64 + c.lane;
-    c.active = Q < a.qrow;
-    c.offL = (Q >> 3) * 64 + (Q & 7) * 4;
-    cu32p elog = (cu32p)a.elog;
+    const uint32_t Qg = slab * G::Q + qt;
+    c.active = Qg < a.qrow;
+    c.offL = (Qg >> 3) * 64 + (Qg & 7) * 4;
 
     uint32_t L[NR], H[NR];
     // IFFT starts with the low k bits (layout A), FFT with the high ones (B).
     constexpr bool START_B = !PT::IFFT;
+    // Final layout: after FFT -> A; after IFFT only -> B (T > 4); T <= 4: A == B.
+    constexpr bool END_B = !PT::FFT && T > 4;
 
     // ---------------- load ----------------
+    constexpr int NZ = PT::LOAD == LD_DEC_LAST ? NR : 1;
+    uint32_t zl[NZ], zh[NZ];
     if constexpr (PT::LOAD == LD_PLAIN) {
 #pragma unroll
         for (int m = 0; m < NR; m++) {
@@ -371,142 +527,129 @@ __global__ void __launch_bounds__(Geo<T>::THREADS) pass_kernel(PassArgs a) {
             else L[m] = H[m] = 0;
         }
     } else if constexpr (PT::LOAD == LD_GATHER_DEC) {
-        // "MULTIPLY SHARDS" of rate_high.rs:203-228 / rate_low.rs:203-228:
-        // received rows * erasure log, everything else zero.
-        uint32_t Y[NR][2];
-        bool got[NR];
+        // received rows (multiplied after the staging barrier), else zero
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            const uint8_t* src = nullptr;
+            L[m] = H[m] = 0;
             if (r < a.a_count) {
-                if (!a.flags_a || uni(((cu8p)a.flags_a)[r])) src = a.seg_a + (uint64_t)r * a.S;
+                if (!a.flags_a || a.flags_a[r]) ld_quad(a.seg_a + (uint64_t)r * a.S, c, L[m], H[m]);
             } else if (r >= a.chunk && r - a.chunk < a.b_count) {
                 const uint32_t i = r - a.chunk;
-                if (!a.flags_b || uni(((cu8p)a.flags_b)[i])) src = a.seg_b + (uint64_t)i * a.S;
-            }
-            got[m] = src != nullptr;
-            if (src) ld_quad(src, c, Y[m][0], Y[m][1]);
-            else Y[m][0] = Y[m][1] = 0;
-        }
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            L[m] = H[m] = 0;
-            if (got[m]) {
-                const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-                uint32_t tt[20];
-                load_table_global(tt, a, uni(elog[r]));
-                mul_xor(L[m], H[m], Y[m][0], Y[m][1], tt);
+                if (!a.flags_b || a.flags_b[i]) ld_quad(a.seg_b + (uint64_t)i * a.S, c, L[m], H[m]);
             }
         }
-    } else {  // LD_DEC_LAST: y = u + L(z)  (formal-derivative part over the tile's bits)
+    } else {  // LD_DEC_LAST: u in registers, z for y = u + L(z)
 #pragma unroll
         for (int m = 0; m < NR; m++) {
-            const uint32_t k = kidx<T, START_B>(c, m);
-            const uint32_t r = row_rel<T>(c, a, k);
-            uint32_t zl, zh;
-            ld_quad(a.in + (uint64_t)r * a.S, c, zl, zh);
-            lds[k * 64 + c.lane] = make_uint2(zl, zh);
+            const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
+            ld_quad(a.in + (uint64_t)r * a.S, c, zl[m], zh[m]);
             ld_quad(a.in2 + (uint64_t)r * a.S, c, L[m], H[m]);
         }
     }
     // Stage the first direction's tables (and, in two-direction programs,
-    // the second direction's layout-B tables); their loads overlap the tile's.
+    // the second direction's layout-B tables, and the decoder's per-row
+    // multipliers); their loads overlap the tile's.
     {
-        const uint32_t skew1 = PT::IFFT ? a.skew_ifft : a.skew_fft;
-        Stager<T, Geo<T>::NTAB> s1;
-        s1.issue(0, 0, skew1, c, a);
+        Stager<T, G::NTAB> s1;
+        s1.issue(a, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
         if constexpr (TWO) {
-            Stager<T, Geo<T>::NTAB - Geo<T>::TSPLIT> s2;
-            s2.issue(Geo<T>::TSPLIT, Geo<T>::TSPLIT, a.skew_fft, c, a);
+            Stager<T, G::NTAB - G::TSPLIT> s2;
+            s2.issue(a, TwiddleEntry<T>{a, c, G::TSPLIT, a.skew_fft});
             s2.commit(tab2);
+        }
+        if constexpr (PT::LOAD == LD_GATHER_DEC) {
+            Stager<T, (1 << T)> se;
+            se.issue(a, GatherEntry<T>{a, c});
+            se.commit(ert);
+        }
+        if constexpr (PT::STORE == ST_RESTORE && !(PT::FFT && T > 4)) {
+            Stager<T, (1 << T)> sr;
+            sr.issue(a, RevealEntry<T>{a, c});
+            const bool lf = threadIdx.x < (1u << T) && row_lost_original(a, row_rel<T>(c, a, threadIdx.x));
+            sr.commit(rvt);
+            if (threadIdx.x < (1u << T)) lostf[threadIdx.x] = lf;
         }
         s1.commit(tab1);
     }
-    __syncthreads();  // staged tables (and DEC_LAST's z tile) visible
-    if constexpr (PT::LOAD == LD_DEC_LAST) {
-        fd_from_lds<T, START_B>(L, H, c, lds);
-        __syncthreads();
+    __syncthreads();  // staged tables visible
+    if constexpr (PT::LOAD == LD_GATHER_DEC) {
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            uint32_t tt[20];
+            load_table_lds(tt, ert + kidx<T, START_B>(c, m) * 5);
+            const uint32_t yl = L[m], yh = H[m];
+            L[m] = H[m] = 0;
+            mul_xor(L[m], H[m], yl, yh, tt);
+        }
     }
+    if constexpr (PT::LOAD == LD_DEC_LAST) tile_fd<T, START_B>(L, H, zl, zh, c, lds);
 
     // ---------------- IFFT ----------------
     bool in_b = START_B;
     if constexpr (PT::IFFT) {
-        layers<T, false, 0, R, false, false>(L, H, c, tab1, tab2);
+        layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
         if constexpr (T > 4) {
-            // stores A -> LDS, barrier, loads B (exchange writes first, so the
-            // layout-A tables are dead after its first barrier)
-            // Second direction's layout-A tables replace the first's (dead
-            // once every wave has passed the exchange barrier below).
-            Stager<T, (TWO ? Geo<T>::TSPLIT : 0)> s3;
-            if constexpr (TWO) s3.issue(0, 0, a.skew_fft, c, a);
-#pragma unroll
-            for (int m = 0; m < NR; m++) lds[kidx<T, false>(c, m) * 64 + c.lane] = make_uint2(L[m], H[m]);
-            __syncthreads();
-            if constexpr (TWO) s3.commit(tab1);
-#pragma unroll
-            for (int m = 0; m < NR; m++) {
-                uint2 v = lds[kidx<T, true>(c, m) * 64 + c.lane];
-                L[m] = v.x;
-                H[m] = v.y;
-            }
-            __syncthreads();
-            layers<T, true, 4, (T > 4 ? T : 4), false, false>(L, H, c, tab1, tab2);
+            // Two-direction programs: the second direction's layout-A tables
+            // replace the first's, which are dead once every wave has passed
+            // the exchange's first barrier.
+            Stager<T, (TWO ? G::TSPLIT : 0)> s3;
+            if constexpr (TWO) s3.issue(a, TwiddleEntry<T>{a, c, 0, a.skew_fft});
+            exchange<T, false>(L, H, c, lds, [&]() {
+                if constexpr (TWO) s3.commit(tab1);
+            });
+            layers<T, true, 4, (T > 4 ? T : 4), false, false>(L, H, c, a, tab1, tab2);
             in_b = true;
         }
     }
     // ---------------- formal derivative (tile bits) ----------------
     if constexpr (PT::FD) {
-        if (in_b) {
-#pragma unroll
-            for (int m = 0; m < NR; m++) lds[kidx<T, true>(c, m) * 64 + c.lane] = make_uint2(L[m], H[m]);
-            __syncthreads();
-            fd_from_lds<T, true>(L, H, c, lds);
-        } else {
-#pragma unroll
-            for (int m = 0; m < NR; m++) lds[kidx<T, false>(c, m) * 64 + c.lane] = make_uint2(L[m], H[m]);
-            __syncthreads();
-            fd_from_lds<T, false>(L, H, c, lds);
-        }
-        __syncthreads();
+        if (in_b) tile_fd<T, true>(L, H, L, H, c, lds);
+        else tile_fd<T, false>(L, H, L, H, c, lds);
     }
     // ---------------- FFT ----------------
     if constexpr (PT::FFT) {
         if constexpr (T > 4) {
-            layers<T, true, 4, (T > 4 ? T : 4), true, TWO>(L, H, c, tab1, tab2);
-            exchange<T, true>(L, H, c, lds);
+            // Reveal multipliers are staged late (T > 4), to keep their
+            // registers out of the load phase.
+            Stager<T, (PT::STORE == ST_RESTORE ? (1 << T) : 0)> sr;
+            bool lf = false;
+            if constexpr (PT::STORE == ST_RESTORE) {
+                sr.issue(a, RevealEntry<T>{a, c});
+                lf = threadIdx.x < (1u << T) && row_lost_original(a, row_rel<T>(c, a, threadIdx.x));
+            }
+            layers<T, true, 4, (T > 4 ? T : 4), true, TWO, PRUNE>(L, H, c, a, tab1, tab2);
+            exchange<T, true>(L, H, c, lds, [&]() {
+                if constexpr (PT::STORE == ST_RESTORE) {
+                    sr.commit(rvt);
+                    if (threadIdx.x < (1u << T)) lostf[threadIdx.x] = lf;
+                }
+            });
             in_b = false;
         }
         // two-direction, T <= 4: the whole second direction is in tab2
-        layers<T, false, 0, R, true, (TWO && T <= 4)>(L, H, c, tab1, tab2);
+        bool need = true;
+        if constexpr (PRUNE) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
+        if (need) layers<T, false, 0, R, true, (TWO && T <= 4)>(L, H, c, a, tab1, tab2);
     }
 
     // ---------------- store ----------------
-    // Final layout: after FFT -> A; after IFFT only -> B (T > 4); T <= 4: A == B.
-    constexpr bool END_B = !PT::FFT && T > 4;
 #pragma unroll
     for (int m = 0; m < NR; m++) {
-        const uint32_t r = row_rel<T>(c, a, kidx<T, END_B>(c, m));
+        const uint32_t k = kidx<T, END_B>(c, m);
+        const uint32_t r = row_rel<T>(c, a, k);
         if constexpr (PT::STORE == ST_PLAIN) {
-            st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
+            if (!PRUNE || (k >= a.need_lo && k < a.need_hi)) st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
         } else if constexpr (PT::STORE == ST_RECOVERY) {
             if (r < a.out_rows) st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
         } else {
-            // REVEAL ERASURES (rate_high.rs:236-242 / rate_low.rs:236-242):
-            // lost original i -> work[i] * (GF_MODULUS - erasures[i]).
-            const uint32_t base = a.rest_seg_b ? a.chunk : 0;
-            const uint32_t cnt = a.rest_seg_b ? a.b_count : a.a_count;
-            const uint8_t* fl = a.rest_seg_b ? a.flags_b : a.flags_a;
-            if (r >= base && r - base < cnt) {
-                const uint32_t i = r - base;
-                const bool received = !fl || uni(((cu8p)fl)[i]);
-                if (!received) {
-                    uint32_t tt[20];
-                    load_table_global(tt, a, GF_MODULUS - uni(elog[r]));
-                    uint32_t ol = 0, oh = 0;
-                    mul_xor(ol, oh, L[m], H[m], tt);
-                    st_quad(a.rest + (uint64_t)i * a.S, c, ol, oh);
-                }
+            if (lostf[k]) {
+                uint32_t tt[20];
+                load_table_lds(tt, rvt + k * 5);
+                uint32_t ol = 0, oh = 0;
+                mul_xor(ol, oh, L[m], H[m], tt);
+                const uint32_t i = r - (a.rest_seg_b ? a.chunk : 0);
+                st_quad(a.rest + (uint64_t)i * a.S, c, ol, oh);
             }
         }
     }
@@ -535,17 +678,27 @@ static const int kSmem[NUM_PROGS][9] = {
 };
 #undef RS16_SM
 
-hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, hipStream_t s) {
+#define RS16_TH(P)                                                                                             \
+    {Geo<0>::THREADS, Geo<1>::THREADS, Geo<2>::THREADS, Geo<3>::THREADS, Geo<4>::THREADS, Geo<5>::THREADS,       \
+     Geo<6>::THREADS, Geo<7>::THREADS, Geo<8>::THREADS}
+static const int kThreads[9] = RS16_TH(0);
+static const int kQuads[9] = {Geo<0>::Q, Geo<1>::Q, Geo<2>::Q, Geo<3>::Q, Geo<4>::Q,
+                              Geo<5>::Q, Geo<6>::Q, Geo<7>::Q, Geo<8>::Q};
+#undef RS16_TH
+
+hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles, hipStream_t s) {
     if (prog < 0 || prog >= NUM_PROGS || T < 0 || T > 8) return hipErrorInvalidValue;
-    if (num_tiles == 0) return hipSuccess;
-    const int W = T > 4 ? (1 << (T - 4)) : 1;
+    if (num_tiles == 0 || args.qrow == 0) return hipSuccess;
+    PassArgs a = args;
+    a.nslab = (a.qrow + kQuads[T] - 1) / kQuads[T];
+    if (a.need_hi == 0) a.need_hi = 1u << T;  // no pruning
     const size_t lds = (size_t)kSmem[prog][T];
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)kPass[prog][T], hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);
         if (e != hipSuccess) return e;
     }
-    dim3 grid(num_tiles * a.nslab), block(64 * W);
+    dim3 grid(num_tiles * a.nslab), block(kThreads[T]);
     hipLaunchKernelGGL(kPass[prog][T], grid, block, lds, s, a);
     return hipGetLastError();
 }

@@ -6,7 +6,7 @@ TAG=${1:-dev}
 cd /tmp && export TMPDIR=/tmp
 OUT="$R/gpurun_out/pmc_$TAG"
 mkdir -p "$OUT"
-ARGS="--steps 5 --warmup 1 --no-cpu-baseline --no-extra"
+ARGS="--steps 5 --warmup 1 --no-cpu-baseline --no-extra ${EXTRA_ARGS:-}"
 if [ "${LIST:-0}" = "1" ]; then rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true; fi
 i=0
 for grp in "${@:2}"; do
