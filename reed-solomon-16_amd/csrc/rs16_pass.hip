@@ -308,10 +308,13 @@ template <int NR> __device__ __forceinline__ void pin_rows(uint32_t (&L)[NR], ui
     }
 }
 
-// PRUNE (layout-B FFT groups of DEC_MID): a group whose rows
-// [gi << (kb+1), (gi+1) << (kb+1)) miss [need_lo, need_hi) feeds no
-// consumed output and is skipped (the condition is uniform).
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, bool PRUNE, int G> struct GroupLoop {
+// PRUNE (layout-B groups of DEC_MID; the condition is uniform):
+//   PR_OUT  FFT: a group whose rows [gi << (kb+1), (gi+1) << (kb+1)) miss
+//           [need_lo, need_hi) feeds no consumed output and is skipped;
+//   PR_ZERO IFFT: a group whose rows all lie at or above kz (the zero
+//           suffix of the input) stays zero and is skipped.
+enum { PR_NONE = 0, PR_OUT, PR_ZERO };
+template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, int G> struct GroupLoop {
     static __device__ __forceinline__ void run(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                                const PassArgs& a, const uint4* tab1, const uint4* tab2,
                                                const uint32_t (&cur)[20]) {
