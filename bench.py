@@ -65,13 +65,29 @@ def free_port():
     return port
 
 
-def pass_bytes(prog: str, k: int, m: int, S: int) -> float:
+def pass_bytes(prog: str, k: int, m: int, S: int, orig_rcv=None, rec_rcv=None) -> float:
     """Algorithmic HBM bytes of one launch of a pass program (rows read + rows
-    written, S bytes each) for a single-chunk high-rate k:m codec."""
+    written, S bytes each) for a single-chunk high-rate k:m codec.  Decode
+    passes follow the received masks (default: the bench's 100 % loss,
+    recovery [0, k) given): a DEC_FIRST tile without a received row is
+    neither read nor written, and its rows are not read again by DEC_MID /
+    DEC_LAST (rs16_pass.hip, "decode zero tiles")."""
+    import numpy as np
+
     chunk = 1 << (m - 1).bit_length()
     n_dec = 1 << (chunk + k - 1).bit_length()
     L_enc, L_dec = chunk.bit_length() - 1, n_dec.bit_length() - 1
     lo_e, lo_d = L_enc // 2, L_dec // 2
+    if orig_rcv is None:
+        orig_rcv = np.zeros(k, bool)
+    if rec_rcv is None:
+        rec_rcv = np.arange(m) < min(k, m)
+    rcv = np.zeros(n_dec, bool)
+    rcv[:m] = rec_rcv
+    rcv[chunk:chunk + k] = orig_rcv
+    tile = 1 << lo_d
+    live = rcv.reshape(-1, tile).any(axis=1)  # DEC_FIRST tiles that are computed and stored
+    t0, t1 = chunk // tile, -(-(chunk + k) // tile)  # DEC_LAST tiles (hold originals)
     if prog == "ENC_FIRST":
         rows = k + chunk
     elif prog == "ENC_MID":
@@ -80,12 +96,11 @@ def pass_bytes(prog: str, k: int, m: int, S: int) -> float:
         tiles_rows = -(-m // (1 << lo_e)) << lo_e
         rows = tiles_rows + m
     elif prog == "DEC_FIRST":
-        rows = k + n_dec  # 100 % loss: k recovery rows read
+        rows = int(rcv.sum()) + int(live.sum()) * tile
     elif prog == "DEC_MID":
-        rows = 2 * n_dec
+        rows = int(live.sum()) * tile + (t1 - t0) * tile
     elif prog == "DEC_LAST":
-        t = -(-k // (1 << lo_d)) << lo_d
-        rows = 2 * t + k
+        rows = (t1 - t0) * tile + int(live[t0:t1].sum()) * tile + int((~orig_rcv).sum())
     elif prog == "ENC_SINGLE":
         rows = k + m
     elif prog == "DEC_SINGLE":
@@ -240,7 +255,7 @@ def main():
     kernels = {name: {"avg_us": ms / n * 1e3, "launches": n} for name, (ms, n) in prof.items()}
     dom = max(prof, key=lambda p: prof[p][0])
     dom_avg_s = prof[dom][0] / prof[dom][1] / 1e3
-    alg = pass_bytes(dom, k, m, S)
+    alg = pass_bytes(dom, k, m, S, of.astype(bool), rf.astype(bool))
     achieved = alg / dom_avg_s / 1e9
     traffic = None
     tp = Path(args.traffic_json)

@@ -200,6 +200,7 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->ws_work32.release();
     e->ws_elog.release();
     e->ws_flags.release();
+    e->ws_zflag.release();
     if (e->d_skew_entry) (void)hipFree(e->d_skew_entry);
     if (e->d_mul_tab) (void)hipFree(e->d_mul_tab);
     if (e->d_log_walsh) (void)hipFree(e->d_log_walsh);

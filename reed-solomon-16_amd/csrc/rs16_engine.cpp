@@ -237,6 +237,10 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_
         return RS16_OK;
     }
     const int lo = L / 2, hi = L - lo;
+    // One flag per DEC_FIRST tile (2^hi <= 256): tiles without a received
+    // row are skipped by DEC_FIRST and read as zero by DEC_MID / DEC_LAST.
+    RS16_HIP(ws_zflag.reserve(256));
+    a.zflags = (uint8_t*)ws_zflag.p;
     a.lo = 0;
     a.out = Z;
     RS16_PASS(DEC_FIRST, lo, a, 1u << hi, s);

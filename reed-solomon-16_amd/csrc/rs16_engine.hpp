@@ -51,6 +51,7 @@ struct rs16_engine {
     uint16_t* d_log_walsh = nullptr;
     // scratch
     rs16::DevBuf ws_z, ws_u, ws_fd, ws_work32, ws_elog, ws_flags;
+    rs16::DevBuf ws_zflag;  // decode: per DEC_FIRST tile, 1 = no received row (tile skipped, rows zero)
 
     hipStream_t pick(void* s) const { return s ? (hipStream_t)s : stream; }
     int activate(rs16_error* err);

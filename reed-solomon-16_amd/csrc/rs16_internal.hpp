@@ -66,6 +66,10 @@ struct PassArgs {
     // consumed downstream; FFT groups and stores outside it are skipped.
     // need_hi == 0: no pruning.
     uint32_t need_lo, need_hi;
+    // Decode zero tiles: zflags[t] = 1 when DEC_FIRST tile t held no received
+    // row (then it is all zero and not stored).  Written by DEC_FIRST, read by
+    // DEC_MID (row r -> flag r >> lo) and DEC_LAST; nullptr: no skipping.
+    uint8_t* zflags;
 };
 
 // Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.

@@ -16,9 +16,10 @@
 //   VGPRs; a wave holds 64/Q row sets.  The 4 layers whose row bits are in
 //   registers are radix-16 butterfly networks with no data movement; LDS
 //   transposes switch between layout A (k bits 0-3 in registers) and layout B
-//   (k bits T-4..T-1).  The transpose runs in NQR rounds of QL quads so that
-//   the LDS image is at most 32 KiB and two or three workgroups share a CU:
-//   one workgroup's HBM loads and stores overlap another's butterflies.
+//   (k bits T-4..T-1).  The transpose runs in NQR rounds of QL quads; NQR is
+//   chosen per program (Rnd below) to bound a workgroup's LDS so that several
+//   workgroups share a CU: one workgroup's HBM loads and stores overlap
+//   another's butterflies.
 //
 //   Twiddle tables: a tile needs 2^T - 1 distinct twiddles per transform
 //   direction (one per (layer, group)).  Their 80-byte v_perm multiply tables
@@ -33,9 +34,19 @@
 //     IFFT layer d: b ^= a;  a ^= b * skew[r + d + skew_delta - 1]
 //   r = group start (row & ~(2d-1)); the GF_MODULUS sentinel ("no multiply",
 //   engine_naive.rs:64,116) maps to the all-zero table ZERO_ENTRY.
+//
+//   Decode zero tiles: a DEC_FIRST tile none of whose rows was received is
+//   all zero after the erasure multiply (rate_high.rs:210-228 zero-fills
+//   every row it does not multiply) and stays zero through its IFFT layers.
+//   It is neither computed nor stored; its flag zflags[tile] = 1 tells
+//   DEC_MID to read those rows as zero and to skip the IFFT groups whose rows
+//   all are, and DEC_LAST that its z term is zero (y = u + L(z) = u).  At
+//   100 % original loss this is the whole original half of the decode work.
 #include "rs16_internal.hpp"
 
 namespace rs16 {
+
+typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
 enum LoadMode { LD_PLAIN = 0, LD_GATHER_ENC, LD_GATHER_DEC, LD_DEC_LAST };
 enum StoreMode { ST_PLAIN = 0, ST_RECOVERY, ST_RESTORE };
@@ -73,38 +84,53 @@ template <int T> struct Geo {
     static constexpr int NTAB = (1 << T) - 1;             // twiddle groups per direction
     // Tables of layers kb >= 4 (layout-B phase) come last: t >= TSPLIT.
     static constexpr int TSPLIT = T > 4 ? (1 << T) - (1 << (T - 4)) : 0;
-    // LDS transposes run in NQR rounds of QL quads (image <= 32 KiB).
-    static constexpr int QL = (4096 >> T) < Q ? (4096 >> T) : Q;
-    static constexpr int NQR = Q / QL;
+};
+
+// LDS rounds of the layout switches at T = 8 / T = 7 (diagnostic builds may
+// override them).  The programs that stage reveal tables (DEC_LAST,
+// DEC_SINGLE) keep 2 rounds at T = 8.
+#ifndef RS16_NQR8
+#define RS16_NQR8 2
+#endif
+#ifndef RS16_NQR7
+#define RS16_NQR7 2
+#endif
+template <int P, int T> struct Rnd {
+    static constexpr int NQR = T == 8 ? (ProgTraits<P>::STORE == ST_RESTORE ? 2 : RS16_NQR8)
+                                      : (T == 7 ? RS16_NQR7 : 1);
+    static constexpr int QL = Geo<T>::Q / NQR;
 };
 
 // Dynamic LDS layout of program P at tile bits T (bytes):
-//   [data image: 2^T x QL x 8][tab1: NTAB x 80][tab2: (NTAB - TSPLIT) x 80]
-//   [ert: 2^T x 80 (gather multipliers)][rvt: 2^T x 80 (reveal multipliers)]
-//   [lost: 2^T x u32 (row is a lost original)]
-// tab1 holds the first direction's tables; in two-direction programs tab2
-// holds the second direction's layout-B tables and its layout-A tables are
-// restaged into tab1 once the first direction's layout-A phase is done.
+//   [region 0: data image 2^T x QL x 8 | gather multipliers 2^T x 80]
+//   [tab1: NTAB x 80][tab2: (NTAB - TSPLIT) x 80]
+//   [rvt: 2^T x 80 (reveal multipliers)][lost: 2^T x u32 (row is a lost original)]
+// The gather multipliers are consumed right after the load, before the first
+// layout switch writes the image (a barrier separates the two).  tab1 holds
+// the first direction's tables; in two-direction programs tab2 holds the
+// second direction's layout-B tables and its layout-A tables are restaged
+// into tab1 once the first direction's layout-A phase is done.
 template <int P, int T> struct Smem {
     using PT = ProgTraits<P>;
     static constexpr bool TWO = PT::IFFT && PT::FFT;
-    static constexpr bool DATA = T > 4 || PT::FD || PT::LOAD == LD_DEC_LAST;
-    static constexpr int DATA_BYTES = DATA ? (1 << T) * Geo<T>::QL * 8 : 0;
+    static constexpr int IMG_BYTES = T > 4 ? (1 << T) * Rnd<P, T>::QL * 8 : 0;
+    static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
+    static constexpr int R0_BYTES = IMG_BYTES > ERT_BYTES ? IMG_BYTES : ERT_BYTES;
     static constexpr int TAB1_BYTES = Geo<T>::NTAB * 80;
     static constexpr int TAB2_BYTES = TWO ? (Geo<T>::NTAB - Geo<T>::TSPLIT) * 80 : 0;
-    static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
     static constexpr int RVT_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 80 : 0;
     static constexpr int LOST_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 4 : 0;
-    static constexpr int TAB1_OFF = DATA_BYTES;
+    static constexpr int ERT_OFF = 0;
+    static constexpr int TAB1_OFF = R0_BYTES;
     static constexpr int TAB2_OFF = TAB1_OFF + TAB1_BYTES;
-    static constexpr int ERT_OFF = TAB2_OFF + TAB2_BYTES;
-    static constexpr int RVT_OFF = ERT_OFF + ERT_BYTES;
+    static constexpr int RVT_OFF = TAB2_OFF + TAB2_BYTES;
     static constexpr int LOST_OFF = RVT_OFF + RVT_BYTES;
     static constexpr int BYTES = LOST_OFF + LOST_BYTES;
 };
 
 struct Thr {
     uint32_t lane, w, s;   // lane, wave, row set
+    uint32_t qt;           // quad within the tile row
     uint32_t ql, round;    // quad within the LDS round, LDS round
     uint32_t b_low, b_high, offL;
     bool active;
@@ -308,16 +334,16 @@ template <int NR> __device__ __forceinline__ void pin_rows(uint32_t (&L)[NR], ui
     }
 }
 
-// PRUNE (layout-B groups of DEC_MID; the condition is uniform):
+// PRUNE (layout-B groups of DEC_MID; the conditions are uniform):
 //   PR_OUT  FFT: a group whose rows [gi << (kb+1), (gi+1) << (kb+1)) miss
 //           [need_lo, need_hi) feeds no consumed output and is skipped;
-//   PR_ZERO IFFT: a group whose rows all lie at or above kz (the zero
-//           suffix of the input) stays zero and is skipped.
+//   PR_ZERO IFFT: a group whose rows are all zero on input stays zero and is
+//           skipped.  zmask bit j = tile rows [16j, 16j+16) are all zero.
 enum { PR_NONE = 0, PR_OUT, PR_ZERO };
 template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, int G> struct GroupLoop {
     static __device__ __forceinline__ void run(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                                const PassArgs& a, const uint4* tab1, const uint4* tab2,
-                                               const uint32_t (&cur)[20]) {
+                                               const uint32_t (&cur)[20], uint32_t zmask) {
         using S = LayerSeq<T, LB, KB0, KB1, FFT>;
         constexpr int s = S::step_of(G), gi = S::index_of(G);
         constexpr int kb = S::kb_of(s);
@@ -328,8 +354,14 @@ template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, i
             load_table_lds(nxt, group_table<T, LB, KB0, KB1, FFT, G + 1, IN_TAB2>(c, tab1, tab2));
         __builtin_amdgcn_sched_barrier(0);  // the prefetch is issued before this group's work
         bool need = true;
-        if constexpr (PRUNE)
+        if constexpr (PRUNE == PR_OUT)
             need = ((uint32_t)gi << (kb + 1)) < a.need_hi && ((uint32_t)(gi + 1) << (kb + 1)) > a.need_lo;
+        if constexpr (PRUNE == PR_ZERO) {
+            static_assert(LB && kb >= 4, "zero pruning works on 16-row blocks of layout B");
+            constexpr int nb = 1 << (kb - 3);  // 16-row blocks covered by the group
+            constexpr uint32_t all = (uint32_t)((1ull << nb) - 1);
+            need = ((zmask >> (gi * nb)) & all) != all;
+        }
         if (need) {
 #pragma unroll
             for (int j = 0; j < (1 << rb); j++) {
@@ -350,58 +382,62 @@ template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, i
 #endif
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (more)
-            GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, G + 1>::run(L, H, c, a, tab1, tab2, nxt);
+            GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, G + 1>::run(L, H, c, a, tab1, tab2, nxt, zmask);
     }
 };
 
 // Apply the layers for k-bits [KB0, KB1) held in registers of layout LB.
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, bool PRUNE = false>
+template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE = PR_NONE>
 __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
-                                       const PassArgs& a, const uint4* tab1, const uint4* tab2) {
+                                       const PassArgs& a, const uint4* tab1, const uint4* tab2,
+                                       uint32_t zmask = 0) {
     if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2)) {
         uint32_t t0[20];
         load_table_lds(t0, group_table<T, LB, KB0, KB1, FFT, 0, IN_TAB2>(c, tab1, tab2));
-        GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0>::run(L, H, c, a, tab1, tab2, t0);
+        GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0>::run(L, H, c, a, tab1, tab2, t0, zmask);
     }
 }
 
 // LDS image of the data: row k, quad ql of the current round.
-template <int T> __device__ __forceinline__ uint2* img(uint2* lds, const Thr& c, uint32_t k) {
-    return lds + k * Geo<T>::QL + c.ql;
+template <int QL> __device__ __forceinline__ uint2* img(uint2* lds, const Thr& c, uint32_t k) {
+    return lds + k * QL + c.ql;
 }
 
-template <int T> __device__ __forceinline__ bool my_round(const Thr& c, int r) {
-    return Geo<T>::NQR == 1 || c.round == (uint32_t)r;
+template <int NQR> __device__ __forceinline__ bool my_round(const Thr& c, int r) {
+    return NQR == 1 || c.round == (uint32_t)r;
 }
 
-template <int T, bool LB>
+template <int T, int QL, bool LB>
 __device__ __forceinline__ void put_rows(const uint32_t (&L)[Geo<T>::NR], const uint32_t (&H)[Geo<T>::NR],
                                          const Thr& c, uint2* lds) {
 #pragma unroll
-    for (int m = 0; m < Geo<T>::NR; m++) *img<T>(lds, c, kidx<T, LB>(c, m)) = make_uint2(L[m], H[m]);
+    for (int m = 0; m < Geo<T>::NR; m++) *img<QL>(lds, c, kidx<T, LB>(c, m)) = make_uint2(L[m], H[m]);
 }
-template <int T, bool LB>
+template <int T, int QL, bool LB>
 __device__ __forceinline__ void get_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                          uint2* lds) {
 #pragma unroll
     for (int m = 0; m < Geo<T>::NR; m++) {
-        const uint2 v = *img<T>(lds, c, kidx<T, LB>(c, m));
+        const uint2 v = *img<QL>(lds, c, kidx<T, LB>(c, m));
         L[m] = v.x;
         H[m] = v.y;
     }
 }
 
-// y[k] ^= XOR_{b < T, k_b = 0} x[k | 2^b] with x read from the LDS image: the
-// formal derivative restricted to the tile's row bits (Engine::formal_derivative,
-// src/engine.rs:233-238, in closed form -- step i = (j & ~(2^b-1)) | 2^b XORs
-// row j|2^b into row j, and that source row is never written before it is read).
-// Row bits held in registers are compile-time: their terms are kept or
-// dropped statically.  Row-set bits differ between lanes: those terms are
-// read unconditionally (for k_b = 1 the address is the row itself) and
-// masked with a select, so all reads of a row issue back to back.
-template <int T, bool LB>
-__device__ __forceinline__ void fd_from_lds(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
-                                            uint2* lds) {
+// y[k] ^= XOR_{b < T, k_b = 0} x[k | 2^b]: the formal derivative restricted
+// to the tile's row bits (Engine::formal_derivative, src/engine.rs:233-238,
+// in closed form -- step i = (j & ~(2^b-1)) | 2^b XORs row j|2^b into row j,
+// and that source row is never written before it is read).
+// Terms of row bits held in registers come straight from registers: rows are
+// updated in ascending m and a term's source row m | 2^b lies above m, so it
+// is read before it is updated and y may alias x.  Terms of row-set bits
+// differ between lanes: they are read from the LDS image of x
+// unconditionally (for k_b = 1 the address is the row itself) and masked
+// with a select, so all reads of a row issue back to back.
+template <int T, int QL, bool LB>
+__device__ __forceinline__ void fd_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR],
+                                        const uint32_t (&SL)[Geo<T>::NR], const uint32_t (&SH)[Geo<T>::NR],
+                                        const Thr& c, uint2* lds) {
     constexpr int R = Geo<T>::R, SHB = Geo<T>::SHB;
 #pragma unroll
     for (int m = 0; m < Geo<T>::NR; m++) {
@@ -414,12 +450,11 @@ __device__ __forceinline__ void fd_from_lds(uint32_t (&L)[Geo<T>::NR], uint32_t 
             if (reg_bit) {
                 const int mb = LB ? b - SHB : b;
                 if (!((m >> mb) & 1)) {
-                    const uint2 v = *img<T>(lds, c, k | (1u << b));
-                    xl ^= v.x;
-                    xh ^= v.y;
+                    xl ^= SL[m | (1 << mb)];
+                    xh ^= SH[m | (1 << mb)];
                 }
             } else {
-                const uint2 v = *img<T>(lds, c, k | (1u << b));
+                const uint2 v = *img<QL>(lds, c, k | (1u << b));
                 const bool take = !((k >> b) & 1);
                 xl ^= take ? v.x : 0u;
                 xh ^= take ? v.y : 0u;
@@ -432,40 +467,43 @@ __device__ __forceinline__ void fd_from_lds(uint32_t (&L)[Geo<T>::NR], uint32_t 
 
 // Layout switch through LDS, in rounds.  `mid` runs after the first barrier
 // (every wave is past its previous phase, so that phase's tables are dead).
-template <int T, bool FROM_B, class MID>
+template <int T, int NQR, bool FROM_B, class MID>
 __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                          uint2* lds, MID mid) {
+    constexpr int QL = Geo<T>::Q / NQR;
     if (RS16_ABLATE == 4) return mid();
 #pragma unroll
-    for (int r = 0; r < Geo<T>::NQR; r++) {
-        if (my_round<T>(c, r)) put_rows<T, FROM_B>(L, H, c, lds);
+    for (int r = 0; r < NQR; r++) {
+        if (my_round<NQR>(c, r)) put_rows<T, QL, FROM_B>(L, H, c, lds);
         __syncthreads();
         if (r == 0) mid();
-        if (my_round<T>(c, r)) get_rows<T, !FROM_B>(L, H, c, lds);
+        if (my_round<NQR>(c, r)) get_rows<T, QL, !FROM_B>(L, H, c, lds);
         __syncthreads();
     }
 }
 
 // y = x + (in-tile formal derivative part) of the rows in registers, where
 // the LDS image is filled from (SL, SH) -- the rows themselves for the
-// (I + H) step of DEC_MID, z for DEC_LAST's y = u + L(z).  In rounds.
-template <int T, bool LB>
+// (I + H) step of DEC_MID, z for DEC_LAST's y = u + L(z).  In rounds; with
+// T <= 4 every row bit is a register bit and no LDS is needed.
+template <int T, int NQR, bool LB>
 __device__ __forceinline__ void tile_fd(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR],
                                         const uint32_t (&SL)[Geo<T>::NR], const uint32_t (&SH)[Geo<T>::NR],
                                         const Thr& c, uint2* lds) {
+    constexpr int QL = Geo<T>::Q / NQR;
     if (RS16_ABLATE == 4) return;
+    if constexpr (T <= 4) {
+        fd_rows<T, QL, LB>(L, H, SL, SH, c, lds);
+    } else {
 #pragma unroll
-    for (int r = 0; r < Geo<T>::NQR; r++) {
-        if (my_round<T>(c, r)) put_rows<T, LB>(SL, SH, c, lds);
-        __syncthreads();
-        if (my_round<T>(c, r)) fd_from_lds<T, LB>(L, H, c, lds);
-        __syncthreads();
+        for (int r = 0; r < NQR; r++) {
+            if (my_round<NQR>(c, r)) put_rows<T, QL, LB>(SL, SH, c, lds);
+            __syncthreads();
+            if (my_round<NQR>(c, r)) fd_rows<T, QL, LB>(L, H, SL, SH, c, lds);
+            __syncthreads();
+        }
     }
 }
-
-struct NoMid {
-    __device__ __forceinline__ void operator()() const {}
-};
 
 template <int P, int T>
 __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pass_kernel(PassArgs a) {
@@ -474,8 +512,10 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
     using G = Geo<T>;
     constexpr int NR = G::NR;
     constexpr int R = G::R;
+    constexpr int NQR = Rnd<P, T>::NQR;
+    constexpr int QL = Rnd<P, T>::QL;
     constexpr bool TWO = SM::TWO;
-    constexpr bool PRUNE = P == DEC_MID;
+    constexpr bool ZERO_SKIP = P == DEC_MID && T > 4;  // DEC_MID runs with T >= 5 only
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint2* lds = (uint2*)smem;
     uint4* tab1 = (uint4*)(smem + SM::TAB1_OFF);
@@ -484,25 +524,33 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
     uint4* rvt = (uint4*)(smem + SM::RVT_OFF);
     uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
 
-    // Block -> (tile, slab): when the grid is a multiple of 8, each XCD
-    // (blocks are dealt to the 8 XCDs round-robin) gets a contiguous range
-    // of (tile, slab), so the slabs of a tile share their twiddle tables in
-    // one L2.
-    const uint32_t nb = gridDim.x, b = blockIdx.x;
-    const uint32_t gid = (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
-    const uint32_t slab = gid % a.nslab;
-    const uint32_t tile = gid / a.nslab + a.tile_base;
+    // Block -> (tile, slab), XCD-aware: blocks are dealt to the 8 XCDs
+    // round-robin (XCD = b mod 8).  With a tile count that is a multiple of 8,
+    // all slabs of a tile run on one XCD (they share their twiddle tables in
+    // its L2) and consecutive tiles go to different XCDs, so tiles of uneven
+    // work (DEC_FIRST zero tiles, pruned rows) spread evenly over the chip.
+    const uint32_t b = blockIdx.x, ntiles = gridDim.x / a.nslab;
+    uint32_t slab, tile;
+    if ((ntiles & 7) == 0) {
+        const uint32_t i = b >> 3;
+        slab = i % a.nslab;
+        tile = (i / a.nslab) * 8 + (b & 7);
+    } else {
+        slab = b % a.nslab;
+        tile = b / a.nslab;
+    }
+    tile += a.tile_base;
 
     Thr c;
     c.lane = threadIdx.x & 63;
     c.w = uni(threadIdx.x >> 6);
-    const uint32_t qt = c.lane % G::Q;
+    c.qt = c.lane % G::Q;
     c.s = c.w * G::HWS + c.lane / G::Q;
-    c.ql = qt % G::QL;
-    c.round = qt / G::QL;
+    c.ql = c.qt % QL;
+    c.round = c.qt / QL;
     c.b_low = tile & ((1u << a.lo) - 1);
     c.b_high = tile >> a.lo;
-    const uint32_t Qg = slab * G::Q + qt;
+    const uint32_t Qg = slab * G::Q + c.qt;
     c.active = Qg < a.qrow;
     c.offL = (Qg >> 3) * 64 + (Qg & 7) * 4;
 
@@ -512,14 +560,36 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
     // Final layout: after FFT -> A; after IFFT only -> B (T > 4); T <= 4: A == B.
     constexpr bool END_B = !PT::FFT && T > 4;
 
+    // ---------------- zero rows of DEC_MID ----------------
+    // Row r of this pass came from DEC_FIRST tile r >> lo = k + (b_high << T).
+    // zrow bit m: this thread's (layout-A) row m is such a skipped, zero row;
+    // zmask bit j: tile rows [16j, 16j+16) all are (uniform, scalar loads).
+    uint32_t zrow = 0, zmask = 0;
+    if constexpr (ZERO_SKIP) {
+        if (a.zflags) {
+            const uint8_t* zt = a.zflags + (c.b_high << T);
+            const uint4 f = *(const uint4*)(zt + (c.s << R));
+            const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+            for (int m = 0; m < NR; m++) zrow |= ((fw[m >> 2] >> (8 * (m & 3))) & 1u) << m;
+            const cu32p zf = (cu32p)zt;
+#pragma unroll
+            for (int j = 0; j < G::SETS; j++)
+                if ((zf[4 * j] & zf[4 * j + 1] & zf[4 * j + 2] & zf[4 * j + 3]) == 0x01010101u) zmask |= 1u << j;
+        }
+    }
+
     // ---------------- load ----------------
     constexpr int NZ = PT::LOAD == LD_DEC_LAST ? NR : 1;
     uint32_t zl[NZ], zh[NZ];
+    bool rcv = false;    // DEC_FIRST: one of this thread's rows was received
+    bool ztile = false;  // DEC_LAST: z of this tile is zero (DEC_FIRST skipped the tile)
     if constexpr (PT::LOAD == LD_PLAIN) {
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a.in + (uint64_t)r * a.S, c, L[m], H[m]);
+            if ((zrow >> m) & 1u) L[m] = H[m] = 0;
+            else ld_quad(a.in + (uint64_t)r * a.S, c, L[m], H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_ENC) {
         // HighRateEncoder::encode: work[0..k) = originals, rest zero (rate_high.rs:50-54)
@@ -536,18 +606,36 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
             L[m] = H[m] = 0;
             if (r < a.a_count) {
-                if (!a.flags_a || a.flags_a[r]) ld_quad(a.seg_a + (uint64_t)r * a.S, c, L[m], H[m]);
+                if (!a.flags_a || a.flags_a[r]) {
+                    rcv = true;
+                    ld_quad(a.seg_a + (uint64_t)r * a.S, c, L[m], H[m]);
+                }
             } else if (r >= a.chunk && r - a.chunk < a.b_count) {
                 const uint32_t i = r - a.chunk;
-                if (!a.flags_b || a.flags_b[i]) ld_quad(a.seg_b + (uint64_t)i * a.S, c, L[m], H[m]);
+                if (!a.flags_b || a.flags_b[i]) {
+                    rcv = true;
+                    ld_quad(a.seg_b + (uint64_t)i * a.S, c, L[m], H[m]);
+                }
             }
         }
     } else {  // LD_DEC_LAST: u in registers, z for y = u + L(z)
+        ztile = a.zflags && a.zflags[tile];
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a.in + (uint64_t)r * a.S, c, zl[m], zh[m]);
+            if (ztile) zl[m] = zh[m] = 0;
+            else ld_quad(a.in + (uint64_t)r * a.S, c, zl[m], zh[m]);
             ld_quad(a.in2 + (uint64_t)r * a.S, c, L[m], H[m]);
+        }
+    }
+    if constexpr (P == DEC_FIRST) {
+        // A tile without received rows is zero after the erasure multiply
+        // and through the IFFT: flag it for DEC_MID / DEC_LAST and stop
+        // before staging anything.
+        const int any = __syncthreads_or(rcv ? 1 : 0);
+        if (a.zflags) {
+            if (slab == 0 && threadIdx.x == 0) a.zflags[tile] = any ? 0 : 1;
+            if (!any) return;
         }
     }
     // Stage the first direction's tables (and, in two-direction programs,
@@ -586,29 +674,37 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
             mul_xor(L[m], H[m], yl, yh, tt);
         }
     }
-    if constexpr (PT::LOAD == LD_DEC_LAST) tile_fd<T, START_B>(L, H, zl, zh, c, lds);
+    if constexpr (PT::LOAD == LD_DEC_LAST) {
+        if (!ztile) tile_fd<T, NQR, START_B>(L, H, zl, zh, c, lds);
+    }
 
     // ---------------- IFFT ----------------
     bool in_b = START_B;
     if constexpr (PT::IFFT) {
-        layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
+        // DEC_MID: a wave whose rows all are zero skips its layout-A layers
+        bool skip_a = false;
+        if constexpr (ZERO_SKIP) skip_a = __all(zrow == (1u << NR) - 1);
+        if (!skip_a) layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
         if constexpr (T > 4) {
             // Two-direction programs: the second direction's layout-A tables
             // replace the first's, which are dead once every wave has passed
             // the exchange's first barrier.
             Stager<T, (TWO ? G::TSPLIT : 0)> s3;
             if constexpr (TWO) s3.issue(a, TwiddleEntry<T>{a, c, 0, a.skew_fft});
-            exchange<T, false>(L, H, c, lds, [&]() {
+            // the gather multipliers share the image's LDS: every wave must be past them
+            if constexpr (PT::LOAD == LD_GATHER_DEC) __syncthreads();
+            exchange<T, NQR, false>(L, H, c, lds, [&]() {
                 if constexpr (TWO) s3.commit(tab1);
             });
-            layers<T, true, 4, (T > 4 ? T : 4), false, false>(L, H, c, a, tab1, tab2);
+            layers<T, true, 4, (T > 4 ? T : 4), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
+                                                                                                tab2, zmask);
             in_b = true;
         }
     }
     // ---------------- formal derivative (tile bits) ----------------
     if constexpr (PT::FD) {
-        if (in_b) tile_fd<T, true>(L, H, L, H, c, lds);
-        else tile_fd<T, false>(L, H, L, H, c, lds);
+        if (in_b) tile_fd<T, NQR, true>(L, H, L, H, c, lds);
+        else tile_fd<T, NQR, false>(L, H, L, H, c, lds);
     }
     // ---------------- FFT ----------------
     if constexpr (PT::FFT) {
@@ -621,8 +717,9 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
                 sr.issue(a, RevealEntry<T>{a, c});
                 lf = threadIdx.x < (1u << T) && row_lost_original(a, row_rel<T>(c, a, threadIdx.x));
             }
-            layers<T, true, 4, (T > 4 ? T : 4), true, TWO, PRUNE>(L, H, c, a, tab1, tab2);
-            exchange<T, true>(L, H, c, lds, [&]() {
+            layers<T, true, 4, (T > 4 ? T : 4), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
+                                                                                             tab2);
+            exchange<T, NQR, true>(L, H, c, lds, [&]() {
                 if constexpr (PT::STORE == ST_RESTORE) {
                     sr.commit(rvt);
                     if (threadIdx.x < (1u << T)) lostf[threadIdx.x] = lf;
@@ -632,7 +729,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
         }
         // two-direction, T <= 4: the whole second direction is in tab2
         bool need = true;
-        if constexpr (PRUNE) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
+        if constexpr (P == DEC_MID) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
         if (need) layers<T, false, 0, R, true, (TWO && T <= 4)>(L, H, c, a, tab1, tab2);
     }
 
@@ -642,7 +739,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
         const uint32_t k = kidx<T, END_B>(c, m);
         const uint32_t r = row_rel<T>(c, a, k);
         if constexpr (PT::STORE == ST_PLAIN) {
-            if (!PRUNE || (k >= a.need_lo && k < a.need_hi)) st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
+            if (P != DEC_MID || (k >= a.need_lo && k < a.need_hi)) st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
         } else if constexpr (PT::STORE == ST_RECOVERY) {
             if (r < a.out_rows) st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
         } else {

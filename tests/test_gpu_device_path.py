@@ -111,3 +111,62 @@ def test_odd_shard_widths(eng, k, m, sb):
     rm = np.zeros(m, bool)
     rm[: k - om.sum()] = True
     assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+
+
+def loss_masks(k, m, pattern):
+    """Received masks for the zero-tile cases: 'all' = every original lost
+    (min(k, m) of them, as benches/benchmarks.rs:82-87 at 100 %); 'blocks' =
+    originals lost in aligned 256-shard blocks, every other block."""
+    om = np.ones(k, bool)
+    if pattern == "all":
+        om[:min(k, m)] = False
+    else:
+        for b in range(0, k, 512):
+            om[b:b + 256] = False
+    lost = int((~om).sum())
+    assert lost <= m
+    rm = np.zeros(m, bool)
+    rm[:lost] = True
+    return om, rm
+
+
+@pytest.mark.parametrize("k,m,sb,pattern", [
+    (32768, 32768, 64, "blocks"),  # 256-row DEC_FIRST tiles: zero tiles between live ones, whole zero 16-tile blocks
+    (4096, 4096, 128, "blocks"),   # 64-row DEC_FIRST tiles, T = 7 DEC_MID
+    (1000, 3000, 1024, "all"),     # low rate: zero prefix of the decode work
+    (3000, 30000, 64, "all"),      # low rate, n = 65536: a whole zero 16-tile block at the start
+    (30000, 3000, 64, "all"),      # high rate, k > m: zero tiles from lost originals and from the zero tail
+])
+def test_decode_zero_tiles(eng, k, m, sb, pattern):
+    # DEC_FIRST tiles without a received row are skipped and read back as
+    # zero by DEC_MID / DEC_LAST (rs16_pass.hip); restoration must be exact.
+    original = generate_original(k, sb, 11)
+    recovery = dev_encode(eng, original, m)
+    assert np.array_equal(recovery, O.encode(k, m, original))
+    om, rm = loss_masks(k, m, pattern)
+    assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+
+
+def test_rate_decoder_zero_tiles():
+    # Same through the work-buffer decoder (src/rate/decoder_work.rs), where the
+    # first pass works in place on the work buffer and skipped tiles keep stale rows.
+    k = m = 4096
+    sb = 128
+    original = generate_original(k, sb, 12)
+    enc = rs16.RateEncoder(k, m, sb, "high")
+    for s in original:
+        enc.add_original_shard(s)
+    with enc.encode() as r:
+        recovery = list(r.recovery_iter())
+    dec = rs16.RateDecoder(k, m, sb, "high")
+    for rnd in range(2):  # second round reuses the work buffer (stale data in lost slots)
+        om, rm = loss_masks(k, m, "blocks" if rnd == 0 else "all")
+        for i in np.flatnonzero(om):
+            dec.add_original_shard(int(i), original[i])
+        for i in np.flatnonzero(rm):
+            dec.add_recovery_shard(int(i), recovery[i])
+        with dec.decode() as res:
+            restored = dict(res.restored_original_iter())
+        assert set(restored) == set(np.flatnonzero(~om).tolist())
+        for i, v in restored.items():
+            assert v == original[i].tobytes(), i
