@@ -295,6 +295,35 @@ def main():
                                    "decode_gib_s": world * (k2 + m2) * S * n2 / td / GIB,
                                    "encode_us": te / n2 * 1e6, "decode_us": td / n2 * 1e6}
 
+    if not args.no_extra:
+        # Shards that start and end in host memory (north_star: recorded beside
+        # the device-resident rate): pinned host buffers, H2D of the inputs,
+        # the same device codec, D2H of the outputs, back to back on one stream.
+        from rs16.device import PinnedArray
+
+        h_orig, h_rec, h_rest = PinnedArray(eng, k * S), PinnedArray(eng, m * S), PinnedArray(eng, k * S)
+        h_orig.array[:] = original.reshape(-1)
+
+        def e2e_encode():
+            h_orig.to_device(d_orig)
+            encode()
+            h_rec.from_device(d_rec)
+
+        def e2e_decode():
+            h_rec.to_device(d_rec, loss * S)
+            decode()
+            h_rest.from_device(d_rest)
+
+        e2e_encode()
+        e2e_decode()
+        assert np.array_equal(h_rest.array.reshape(k, S), original), "host-resident decode did not restore"
+        n3 = max(3, args.steps // 4)
+        te, td = timed(e2e_encode, n3), timed(e2e_decode, n3)
+        extra["host_resident_pcie"] = {
+            "encode_gib_s": world * (k + m) * S * n3 / te / GIB, "decode_gib_s": world * (k + m) * S * n3 / td / GIB,
+            "encode_us": te / n3 * 1e6, "decode_us": td / n3 * 1e6,
+            "path": "pinned host -> hipMemcpyAsync H2D -> device codec -> D2H -> pinned host, sequential on one stream"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(original, recovery, k, m, S, args.cpu_seconds)

@@ -187,6 +187,11 @@ void rs16_device_free(rs16_engine* eng, void* d_ptr);
 int rs16_memcpy_htod(rs16_engine* eng, void* d_dst, const void* src, size_t bytes, void* stream, rs16_error* err);
 int rs16_memcpy_dtoh(rs16_engine* eng, void* dst, const void* d_src, size_t bytes, void* stream, rs16_error* err);
 int rs16_memset_device(rs16_engine* eng, void* d_dst, int value, size_t bytes, void* stream, rs16_error* err);
+/* Page-locked host staging memory (hipHostMalloc): shards that start and end
+ * in host memory move over PCIe at DMA rate from/to these buffers (the
+ * host-resident path of EncoderWork / DecoderWork, src/rate/encoder_work.rs:49-69). */
+void* rs16_host_alloc(rs16_engine* eng, size_t bytes, rs16_error* err);
+void rs16_host_free(rs16_engine* eng, void* h_ptr);
 
 /* Diagnostics: per-kernel timing.  When enabled, every HBM pass (and the
  * eval_poly kernel group) is bracketed by hipEvents on its launch stream.

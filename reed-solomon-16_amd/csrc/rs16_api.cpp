@@ -584,6 +584,19 @@ extern "C" void rs16_device_free(rs16_engine* e, void* p) {
     (void)hipSetDevice(e->device);
     (void)hipFree(p);
 }
+extern "C" void* rs16_host_alloc(rs16_engine* e, size_t bytes, rs16_error* err) {
+    if (e->activate(err)) return nullptr;
+    void* p = nullptr;
+    hipError_t he = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    if (he != hipSuccess) return hip_fail(err, he), nullptr;
+    set_error(err, RS16_OK);
+    return p;
+}
+extern "C" void rs16_host_free(rs16_engine* e, void* p) {
+    if (!p) return;
+    (void)hipSetDevice(e->device);
+    (void)hipHostFree(p);
+}
 extern "C" int rs16_memcpy_htod(rs16_engine* e, void* dst, const void* src, size_t bytes, void* stream,
                                 rs16_error* err) {
     if (int rc = e->activate(err)) return rc;

@@ -46,3 +46,35 @@ class DeviceArray:
                 lib().rs16_device_free(self.engine.h, self.ptr)
         except Exception:
             pass
+
+
+class PinnedArray:
+    """Page-locked host buffer (rs16_host_alloc) viewed as a numpy uint8 array."""
+
+    def __init__(self, engine: Engine, nbytes: int):
+        self.engine, self.nbytes = engine, nbytes
+        err = RS16Error()
+        self.ptr = lib().rs16_host_alloc(engine.h, max(nbytes, 1), C.byref(err))
+        if not self.ptr:
+            raise Error._from_c(err)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(nbytes, 1)).from_address(self.ptr))[:nbytes]
+
+    def to_device(self, d: "DeviceArray", nbytes: int = None):
+        err = RS16Error()
+        if lib().rs16_memcpy_htod(self.engine.h, d.ptr, self.ptr, self.nbytes if nbytes is None else nbytes, None,
+                                  C.byref(err)):
+            raise Error._from_c(err)
+
+    def from_device(self, d: "DeviceArray", nbytes: int = None):
+        err = RS16Error()
+        if lib().rs16_memcpy_dtoh(self.engine.h, self.ptr, d.ptr, self.nbytes if nbytes is None else nbytes, None,
+                                  C.byref(err)):
+            raise Error._from_c(err)
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self.array = None
+                lib().rs16_host_free(self.engine.h, self.ptr)
+        except Exception:
+            pass

@@ -28,7 +28,7 @@ if [ "${SKIP_UBENCH:-0}" != 1 ]; then
   done
 fi
 B="--steps 20 --warmup 5 --no-cpu-baseline --no-extra"
-for v in ${VARIANTS:-ab1 ab2 ab3 ab4}; do
+for v in ${VARIANTS-ab1 ab2 ab3 ab4}; do
   step "ablation $v"
   RS16_LIB="$R/reed-solomon-16_amd/build_$v/librs16.so" timeout -k 10 240 python bench.py $B --no-verify \
       > "$O/$v.json" 2> "$O/$v.err" || fail $v "$O/$v.err"
