@@ -181,6 +181,23 @@ int rs16_decode_device(rs16_engine* eng, size_t original_count, size_t recovery_
                        const uint8_t* d_recovery_received, size_t original_received_count,
                        size_t recovery_received_count, void* stream, rs16_error* err);
 
+/* ---- Host-resident one-shot codec ---------------------------------------
+ * reed_solomon_16::encode / decode (src/lib.rs:242-344) with every shard in
+ * host memory (page-locked, rs16_host_alloc, for DMA-rate copies; pageable
+ * works too).  The shard columns are processed in slices of slice_bytes (a
+ * multiple of 64; 0 = the whole shard) that alternate between two streams,
+ * so that the host->device copy of one slice, the device codec of another
+ * and the device->host copy of a third may overlap (on MI355X the pitched
+ * copies of narrow slices cost more than the overlap gains; see
+ * DESIGN.md).  Synchronous: returns when the
+ * outputs are in host memory.  Decode: received flags are host byte arrays;
+ * lost originals are restored in place into h_original. */
+int rs16_encode_host(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                     const void* h_original, void* h_recovery, size_t slice_bytes, rs16_error* err);
+int rs16_decode_host(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                     void* h_original, const uint8_t* original_received, const void* h_recovery,
+                     const uint8_t* recovery_received, size_t slice_bytes, rs16_error* err);
+
 /* ---- Device memory helpers (so FFI callers need no HIP headers) ------- */
 void* rs16_device_alloc(rs16_engine* eng, size_t bytes, rs16_error* err);
 void rs16_device_free(rs16_engine* eng, void* d_ptr);

@@ -204,6 +204,14 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* 
 int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
                               const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                               hipStream_t s, rs16_error* err) {
+    if (int rc = decode_eval(g, flags_a, flags_b, s, err)) return rc;
+    RS16_HIP(ws_zflag.reserve(256));
+    return decode_passes(g, S, seg_a, flags_a, seg_b, flags_b, rest, Z, U, (uint8_t*)ws_zflag.p, s, err);
+}
+
+// Erasure logs e = eval_poly(erasure vector) into ws_elog (3 small kernels).
+int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
+                             rs16_error* err) {
     RS16_HIP(ws_work32.reserve(GF_ORDER * 4));
     RS16_HIP(ws_elog.reserve(GF_ORDER * 4));
     ErasureSpec es;
@@ -217,8 +225,14 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
     RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s));
-    if (int rc = prof_end(NUM_PROGS, s, ev, err)) return rc;
+    return prof_end(NUM_PROGS, s, ev, err);
+}
 
+// The pass sequence of a decode, given the erasure logs in ws_elog and a
+// 256-byte zero-tile flag buffer of the caller's.
+int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+                               const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
+                               uint8_t* zflags, hipStream_t s, rs16_error* err) {
     PassArgs a = base_args(this, S);
     a.seg_a = seg_a;
     a.seg_b = seg_b;
@@ -239,8 +253,7 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_
     const int lo = L / 2, hi = L - lo;
     // One flag per DEC_FIRST tile (2^hi <= 256): tiles without a received
     // row are skipped by DEC_FIRST and read as zero by DEC_MID / DEC_LAST.
-    RS16_HIP(ws_zflag.reserve(256));
-    a.zflags = (uint8_t*)ws_zflag.p;
+    a.zflags = zflags;
     a.lo = 0;
     a.out = Z;
     RS16_PASS(DEC_FIRST, lo, a, 1u << hi, s);

@@ -52,6 +52,19 @@ struct rs16_engine {
     // scratch
     rs16::DevBuf ws_z, ws_u, ws_fd, ws_work32, ws_elog, ws_flags;
     rs16::DevBuf ws_zflag;  // decode: per DEC_FIRST tile, 1 = no received row (tile skipped, rows zero)
+    // Host-resident pipeline (rs16_encode_host / rs16_decode_host): column
+    // slices alternate between two slots, each with its own stream and the
+    // device buffers of one slice, so copies and compute of different slices
+    // overlap.  hflags: the received flags of a host decode; hev orders the
+    // slots after the engine stream.
+    struct HostSlot {
+        hipStream_t s = nullptr;
+        rs16::DevBuf orig, rec, z, u, zflag;
+    };
+    HostSlot hslot[2];
+    rs16::DevBuf hflags;
+    hipEvent_t hev = nullptr;
+    int host_slots(rs16_error* err);
 
     hipStream_t pick(void* s) const { return s ? (hipStream_t)s : stream; }
     int activate(rs16_error* err);
@@ -86,6 +99,12 @@ struct rs16_engine {
     int decode_fused(const rs16::DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
                      const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                      hipStream_t s, rs16_error* err);
+    // decode_fused = decode_eval (erasure logs into ws_elog) + decode_passes.
+    int decode_eval(const rs16::DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
+                    rs16_error* err);
+    int decode_passes(const rs16::DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+                      const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
+                      uint8_t* zflags, hipStream_t s, rs16_error* err);
     // Generic (engine-op sequence) encoders, following the reference rate code.
     int encode_high_generic(size_t k, size_t m, size_t S, uint8_t* work, size_t work_count, hipStream_t s,
                             rs16_error* err);

@@ -535,3 +535,33 @@ def decode_device(original_count, recovery_count, shard_bytes, d_original, d_ori
                                     Engine._ptr(d_original_received), Engine._ptr(d_recovery),
                                     Engine._ptr(d_recovery_received), original_received_count,
                                     recovery_received_count, stream, C.byref(err)), err)
+
+
+def _host_ptr(x) -> int:
+    """Address of a host buffer: an int (e.g. PinnedArray.ptr) or a C-contiguous numpy array."""
+    if isinstance(x, int):
+        return x
+    if not x.flags["C_CONTIGUOUS"]:
+        raise ValueError("host buffers must be C-contiguous")
+    return x.ctypes.data
+
+
+def encode_host(original_count, recovery_count, shard_bytes, h_original, h_recovery, slice_bytes=0,
+                engine: Optional[Engine] = None):
+    """reed_solomon_16::encode (src/lib.rs:242-279) with shards in host memory
+    (rs16_encode_host: column slices pipelined over two streams)."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_encode_host(eng.h, original_count, recovery_count, shard_bytes, _host_ptr(h_original),
+                                  _host_ptr(h_recovery), slice_bytes, C.byref(err)), err)
+
+
+def decode_host(original_count, recovery_count, shard_bytes, h_original, original_received, h_recovery,
+                recovery_received, slice_bytes=0, engine: Optional[Engine] = None):
+    """reed_solomon_16::decode (src/lib.rs:287-344) with shards in host memory;
+    lost originals are restored in place into h_original (rs16_decode_host)."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_decode_host(eng.h, original_count, recovery_count, shard_bytes, _host_ptr(h_original),
+                                  _host_ptr(original_received), _host_ptr(h_recovery),
+                                  _host_ptr(recovery_received), slice_bytes, C.byref(err)), err)

@@ -80,6 +80,8 @@ SIGNATURES = {
     "rs16_memcpy_htod": (_i, [_p, _p, _p, _sz, _p, _e]),
     "rs16_memcpy_dtoh": (_i, [_p, _p, _p, _sz, _p, _e]),
     "rs16_memset_device": (_i, [_p, _p, _i, _sz, _p, _e]),
+    "rs16_encode_host": (_i, [_p, _sz, _sz, _sz, _p, _p, _sz, _e]),
+    "rs16_decode_host": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _p, _sz, _e]),
     "rs16_host_alloc": (_p, [_p, _sz, _e]),
     "rs16_host_free": (None, [_p, _p]),
 }
