@@ -492,7 +492,9 @@ extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
     if (d->orig_recv == d->k) return set_error(err, RS16_OK);  // nothing to do
     rs16_engine* e = d->eng;
     if (int rc = e->activate(err)) return rc;
-    const DecodeGeom g = decode_geom(d->high, d->k, d->m);
+    DecodeGeom g = decode_geom(d->high, d->k, d->m);
+    g.a_recv = d->high ? d->rec_recv : d->orig_recv;
+    g.b_recv = d->high ? d->orig_recv : d->rec_recv;
     // Received flags of the two segments -> device (bytes, one per row).
     uint8_t* fl = (uint8_t*)d->flags.p;
     RS16_HIP(hipMemcpyAsync(fl, d->received.data(), g.a_count, hipMemcpyHostToDevice, e->stream));
@@ -616,7 +618,9 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
     if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
     if (orig_recv == k) return set_error(err, RS16_OK);
     if (int rc = e->activate(err)) return rc;
-    const DecodeGeom g = decode_geom(high, k, m);
+    DecodeGeom g = decode_geom(high, k, m);
+    g.a_recv = high ? rec_recv : orig_recv;
+    g.b_recv = high ? orig_recv : rec_recv;
     const size_t W = host_slice(S, slice_bytes);
     for (auto& sl : e->hslot) {
         RS16_HIP(sl.orig.reserve(k * W));
@@ -667,7 +671,9 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     if (orig_recv == k) return set_error(err, RS16_OK);
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);
-    const DecodeGeom g = decode_geom(high, k, m);
+    DecodeGeom g = decode_geom(high, k, m);
+    g.a_recv = high ? rec_recv : orig_recv;
+    g.b_recv = high ? orig_recv : rec_recv;
     RS16_HIP(e->ws_z.reserve((size_t)g.n * S));
     RS16_HIP(e->ws_u.reserve((size_t)g.n * S));
     const uint8_t* orig = (const uint8_t*)d_original;

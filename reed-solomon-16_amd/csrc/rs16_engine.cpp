@@ -254,9 +254,24 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg
     // One flag per DEC_FIRST tile (2^hi <= 256): tiles without a received
     // row are skipped by DEC_FIRST and read as zero by DEC_MID / DEC_LAST.
     a.zflags = zflags;
+    // Launch only the tiles that can hold a received row: a segment with no
+    // received shard contributes none (its tiles are flagged by block 0).
+    const uint32_t tile = 1u << lo, ntiles = 1u << hi;
+    uint32_t t0z = ntiles, t1z = 0;
+    if (g.a_recv) t0z = 0, t1z = (g.a_count + tile - 1) / tile;
+    if (g.b_recv) {
+        t0z = std::min(t0z, g.chunk / tile);
+        t1z = std::max(t1z, std::min(ntiles, (uint32_t)(((size_t)g.chunk + g.b_count + tile - 1) / tile)));
+    }
+    if (t1z <= t0z) t0z = 0, t1z = 1;  // (unreachable: a decode has received shards) keep one launch
+    a.zt_lo = t0z;
+    a.zt_hi = t1z;
+    a.ztiles = ntiles;
+    a.tile_base = t0z;
     a.lo = 0;
     a.out = Z;
-    RS16_PASS(DEC_FIRST, lo, a, 1u << hi, s);
+    RS16_PASS(DEC_FIRST, lo, a, t1z - t0z, s);
+    a.tile_base = 0;
     // Only tiles that contain original rows are needed in the last pass,
     // so DEC_MID computes and stores only U rows of those tiles (its tile
     // row k is row bits [lo, L) = the last pass's tile index).

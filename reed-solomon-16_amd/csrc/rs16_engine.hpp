@@ -38,6 +38,9 @@ inline int ilog2(size_t x) { int l = 0; while (((size_t)1 << l) < x) l++; return
 struct DecodeGeom {
     bool high;
     uint32_t a_count, chunk, b_count, n;
+    // Received shard counts of the two segments when the caller knows them
+    // (0: the whole segment is lost, so its first-pass tiles need no launch).
+    size_t a_recv = 1, b_recv = 1;
 };
 DecodeGeom decode_geom(bool high, size_t k, size_t m);
 

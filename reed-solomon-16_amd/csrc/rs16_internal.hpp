@@ -70,6 +70,10 @@ struct PassArgs {
     // row (then it is all zero and not stored).  Written by DEC_FIRST, read by
     // DEC_MID (row r -> flag r >> lo) and DEC_LAST; nullptr: no skipping.
     uint8_t* zflags;
+    // DEC_FIRST is launched on tiles [zt_lo, zt_hi) only (the others cannot
+    // hold a received row: their whole segment was lost); block 0 flags the
+    // rest of the ztiles tiles as zero.
+    uint32_t zt_lo, zt_hi, ztiles;
 };
 
 // Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.

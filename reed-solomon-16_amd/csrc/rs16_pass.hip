@@ -398,10 +398,16 @@ __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[
     }
 }
 
-// LDS image of the data: row k, quad ql of the current round.
-template <int QL> __device__ __forceinline__ uint2* img(uint2* lds, const Thr& c, uint32_t k) {
-    return lds + k * QL + c.ql;
-}
+// LDS image of the data: row k, quad ql of the current round, as two planes
+// (lo dwords, then hi dwords, PLANE dwords apart) so that a row's two dwords
+// go through one ds_write2st64_b32 / ds_read2st64_b32 from independent
+// registers (an interleaved uint2 image needs register pairs: v_mov copies).
+template <int T, int QL> struct Img {
+    static constexpr int PLANE = (1 << T) * QL;
+    static __device__ __forceinline__ uint32_t* at(uint2* lds, const Thr& c, uint32_t k) {
+        return (uint32_t*)lds + k * QL + c.ql;
+    }
+};
 
 template <int NQR> __device__ __forceinline__ bool my_round(const Thr& c, int r) {
     return NQR == 1 || c.round == (uint32_t)r;
@@ -411,16 +417,20 @@ template <int T, int QL, bool LB>
 __device__ __forceinline__ void put_rows(const uint32_t (&L)[Geo<T>::NR], const uint32_t (&H)[Geo<T>::NR],
                                          const Thr& c, uint2* lds) {
 #pragma unroll
-    for (int m = 0; m < Geo<T>::NR; m++) *img<QL>(lds, c, kidx<T, LB>(c, m)) = make_uint2(L[m], H[m]);
+    for (int m = 0; m < Geo<T>::NR; m++) {
+        uint32_t* p = Img<T, QL>::at(lds, c, kidx<T, LB>(c, m));
+        p[0] = L[m];
+        p[Img<T, QL>::PLANE] = H[m];
+    }
 }
 template <int T, int QL, bool LB>
 __device__ __forceinline__ void get_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                          uint2* lds) {
 #pragma unroll
     for (int m = 0; m < Geo<T>::NR; m++) {
-        const uint2 v = *img<QL>(lds, c, kidx<T, LB>(c, m));
-        L[m] = v.x;
-        H[m] = v.y;
+        const uint32_t* p = Img<T, QL>::at(lds, c, kidx<T, LB>(c, m));
+        L[m] = p[0];
+        H[m] = p[Img<T, QL>::PLANE];
     }
 }
 
@@ -454,10 +464,11 @@ __device__ __forceinline__ void fd_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
                     xh ^= SH[m | (1 << mb)];
                 }
             } else {
-                const uint2 v = *img<QL>(lds, c, k | (1u << b));
+                const uint32_t* p = Img<T, QL>::at(lds, c, k | (1u << b));
+                const uint32_t vl = p[0], vh = p[Img<T, QL>::PLANE];
                 const bool take = !((k >> b) & 1);
-                xl ^= take ? v.x : 0u;
-                xh ^= take ? v.y : 0u;
+                xl ^= take ? vl : 0u;
+                xh ^= take ? vh : 0u;
             }
         }
         L[m] = xl;
@@ -629,6 +640,9 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
         }
     }
     if constexpr (P == DEC_FIRST) {
+        if (blockIdx.x == 0 && a.zflags)  // tiles not launched: their segment was lost whole
+            for (uint32_t t = threadIdx.x; t < a.ztiles; t += G::THREADS)
+                if (t < a.zt_lo || t >= a.zt_hi) a.zflags[t] = 1;
         // A tile without received rows is zero after the erasure multiply
         // and through the IFFT: flag it for DEC_MID / DEC_LAST and stop
         // before staging anything.
