@@ -224,7 +224,11 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.tail_fill = g.high ? 0 : 1;
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
-    RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s));
+    // 65536-row decodes run their first and last passes on 256-row tiles,
+    // which finish eval_poly's last 256-point FWHT themselves.
+    elog_fused = ilog2(g.n) == 16;
+    RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s,
+                                         !elog_fused));
     return prof_end(NUM_PROGS, s, ev, err);
 }
 
@@ -242,6 +246,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg
     a.chunk = g.chunk;
     a.b_count = g.b_count;
     a.elog = (const uint32_t*)ws_elog.p;
+    a.ework = elog_fused ? (const uint32_t*)ws_work32.p : nullptr;
     a.rest = rest;
     a.rest_seg_b = g.high ? 1 : 0;
     a.skew_ifft = a.skew_fft = 0;

@@ -78,6 +78,7 @@ struct rs16_engine {
     int prof_begin(hipStream_t s, hipEvent_t* ev, rs16_error* err);
     int prof_end(int id, hipStream_t s, hipEvent_t ev, rs16_error* err);
     bool profiling = false;
+    bool elog_fused = false;  // last decode_eval left the final 256-point FWHT to the passes (ws_work32)
     struct ProfRec {
         int id;
         hipEvent_t a, b;

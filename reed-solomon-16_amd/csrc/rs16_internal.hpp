@@ -74,6 +74,10 @@ struct PassArgs {
     // hold a received row: their whole segment was lost); block 0 flags the
     // rest of the ztiles tiles as zero.
     uint32_t zt_lo, zt_hi, ztiles;
+    // eval_poly with its last 256-point FWHT (row bits 0-7) left undone
+    // (launch_eval_poly_from_flags, last_lo = false): DEC_FIRST / DEC_LAST at
+    // T = 8 finish it for their tile's rows in LDS.  nullptr: use elog.
+    const uint32_t* ework;
 };
 
 // Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.
@@ -93,7 +97,7 @@ struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.r
     uint32_t tail_fill;        // value of rows >= chunk + b_count (1 for low rate)
 };
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
-                                       const uint16_t* log_walsh, hipStream_t s);
+                                       const uint16_t* log_walsh, hipStream_t s, bool last_lo);
 hipError_t launch_eval_poly_u16(uint16_t* data, uint32_t* work, const uint16_t* log_walsh, hipStream_t s);
 hipError_t launch_fwht_u16(uint16_t* data, uint32_t* work, hipStream_t s);
 

@@ -139,11 +139,38 @@ __global__ void __launch_bounds__(256) fwht_lo_kernel(const uint32_t* in32, cons
     else out32[idx] = s[threadIdx.x];
 }
 
+// Contiguous 256-point FWHT of the erasure vector built from the received flags.
+__global__ void __launch_bounds__(256) fwht_lo_flags_kernel(ErasureSpec e, uint32_t* out32) {
+    __shared__ uint32_t s[256];
+    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+    s[threadIdx.x] = erasure_at(e, idx);
+    fwht256_lds(s);
+    out32[idx] = s[threadIdx.x];
+}
+// Strided 256-point FWHT (row bits 8-15), x LogWalsh mod 65535, and again.
+__global__ void __launch_bounds__(256) fwht_hi_mulw_kernel(const uint32_t* in32, uint32_t* out32,
+                                                           const uint16_t* log_walsh) {
+    __shared__ uint32_t s[256];
+    const uint32_t idx = blockIdx.x + 256u * threadIdx.x;
+    s[threadIdx.x] = in32[idx];
+    fwht256_lds(s);
+    s[threadIdx.x] = (uint32_t)(((uint64_t)s[threadIdx.x] * log_walsh[idx]) % GF_MODULUS);
+    fwht256_lds(s);
+    out32[idx] = s[threadIdx.x];
+}
+
+// eval_poly(e) = FWHT(LogWalsh . FWHT(e)) with FWHT = H_lo H_hi (row bits 0-7
+// and 8-15; the two commute): H_lo(e) from the flags, then H_hi . LW . H_hi,
+// then the last H_lo.  With last_lo == false the last H_lo is left to the
+// consumer: the 65536-row decode passes (256-row tiles = one H_lo block each)
+// finish it per tile in LDS (rs16_pass.hip), saving a kernel.
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
-                                       const uint16_t* log_walsh, hipStream_t s) {
-    hipLaunchKernelGGL((fwht_hi_kernel<1, 0>), dim3(256), dim3(256), 0, s, e, nullptr, nullptr, work, nullptr);
-    hipLaunchKernelGGL((fwht_lo_kernel<true, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, work, nullptr, log_walsh);
-    hipLaunchKernelGGL((fwht_hi_kernel<0, 0>), dim3(256), dim3(256), 0, s, e, work, nullptr, out_elog, nullptr);
+                                       const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
+    hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(256), 0, s, e, work);
+    hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(256), 0, s, work, work, log_walsh);
+    if (last_lo)
+        hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
+                           nullptr);
     return hipGetLastError();
 }
 hipError_t launch_eval_poly_u16(uint16_t* data, uint32_t* work, const uint16_t* log_walsh, hipStream_t s) {

@@ -125,7 +125,10 @@ template <int P, int T> struct Smem {
     static constexpr int TAB2_OFF = TAB1_OFF + TAB1_BYTES;
     static constexpr int RVT_OFF = TAB2_OFF + TAB2_BYTES;
     static constexpr int LOST_OFF = RVT_OFF + RVT_BYTES;
-    static constexpr int BYTES = LOST_OFF + LOST_BYTES;
+    // erasure logs of the tile's rows when the pass finishes eval_poly (ework)
+    static constexpr int ELOG_BYTES = ((P == DEC_FIRST || P == DEC_LAST) && T == 8) ? 256 * 4 : 0;
+    static constexpr int ELOG_OFF = LOST_OFF + LOST_BYTES;
+    static constexpr int BYTES = ELOG_OFF + ELOG_BYTES;
 };
 
 struct Thr {
@@ -260,12 +263,15 @@ __device__ __forceinline__ bool row_lost_original(const PassArgs& a, uint32_t r)
 
 // "MULTIPLY SHARDS" of rate_high.rs:203-228 / rate_low.rs:203-228: received
 // row r is multiplied by erasure log e[r]; absent rows by zero.
+// e[r]: from the tile's LDS copy when the pass finished eval_poly itself
+// (el = the tile's 2^T logs), else from HBM.
 template <int T> struct GatherEntry {
     const PassArgs& a;
     const Thr& c;
+    const uint32_t* el;
     __device__ __forceinline__ uint32_t operator()(int k) const {
         const uint32_t r = row_rel<T>(c, a, (uint32_t)k);
-        return row_received(a, r) ? a.elog[r] : ZERO_ENTRY;
+        return row_received(a, r) ? (el ? el[k] : a.elog[r]) : ZERO_ENTRY;
     }
 };
 // REVEAL ERASURES (rate_high.rs:236-242 / rate_low.rs:236-242): lost
@@ -273,11 +279,30 @@ template <int T> struct GatherEntry {
 template <int T> struct RevealEntry {
     const PassArgs& a;
     const Thr& c;
+    const uint32_t* el;
     __device__ __forceinline__ uint32_t operator()(int k) const {
         const uint32_t r = row_rel<T>(c, a, (uint32_t)k);
-        return row_lost_original(a, r) ? GF_MODULUS - a.elog[r] : ZERO_ENTRY;
+        return row_lost_original(a, r) ? GF_MODULUS - (el ? el[k] : a.elog[r]) : ZERO_ENTRY;
     }
 };
+
+// The last 256-point FWHT of eval_poly (src/engine.rs:207-218; row bits 0-7,
+// add/sub mod 65535 as NoSimd::fwht_private, src/engine/engine_nosimd.rs:153-183)
+// over a 256-row tile's values in LDS; every thread of the workgroup calls it.
+__device__ __forceinline__ void fwht256_tile(uint32_t* s) {
+    const uint32_t t = threadIdx.x;
+#pragma unroll
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        __syncthreads();
+        if (t < 128) {
+            const uint32_t i = (t / d) * 2 * d + (t % d), j = i + d;
+            const uint32_t x = s[i], y = s[j];
+            s[i] = add_mod(x, y);
+            s[j] = sub_mod(x, y);
+        }
+    }
+    __syncthreads();
+}
 
 // Layers for k-bits [KB0, KB1) held in registers of layout LB, as a
 // compile-time sequence of twiddle groups (step s, index gi).
@@ -652,6 +677,17 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
             if (!any) return;
         }
     }
+    // Erasure logs of this tile's rows: the last 256-point FWHT of eval_poly,
+    // done here when the caller left it undone (ework); overlaps the tile loads.
+    const uint32_t* el = nullptr;
+    if constexpr (SM::ELOG_BYTES > 0) {
+        if (a.ework) {
+            uint32_t* elds = (uint32_t*)(smem + SM::ELOG_OFF);
+            if (threadIdx.x < 256) elds[threadIdx.x] = a.ework[(tile << 8) + threadIdx.x];
+            fwht256_tile(elds);
+            el = elds;
+        }
+    }
     // Stage the first direction's tables (and, in two-direction programs,
     // the second direction's layout-B tables, and the decoder's per-row
     // multipliers); their loads overlap the tile's.
@@ -665,12 +701,12 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
         }
         if constexpr (PT::LOAD == LD_GATHER_DEC) {
             Stager<T, (1 << T)> se;
-            se.issue(a, GatherEntry<T>{a, c});
+            se.issue(a, GatherEntry<T>{a, c, el});
             se.commit(ert);
         }
         if constexpr (PT::STORE == ST_RESTORE && !(PT::FFT && T > 4)) {
             Stager<T, (1 << T)> sr;
-            sr.issue(a, RevealEntry<T>{a, c});
+            sr.issue(a, RevealEntry<T>{a, c, el});
             const bool lf = threadIdx.x < (1u << T) && row_lost_original(a, row_rel<T>(c, a, threadIdx.x));
             sr.commit(rvt);
             if (threadIdx.x < (1u << T)) lostf[threadIdx.x] = lf;
@@ -728,7 +764,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
             Stager<T, (PT::STORE == ST_RESTORE ? (1 << T) : 0)> sr;
             bool lf = false;
             if constexpr (PT::STORE == ST_RESTORE) {
-                sr.issue(a, RevealEntry<T>{a, c});
+                sr.issue(a, RevealEntry<T>{a, c, el});
                 lf = threadIdx.x < (1u << T) && row_lost_original(a, row_rel<T>(c, a, threadIdx.x));
             }
             layers<T, true, 4, (T > 4 ? T : 4), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
