@@ -489,11 +489,23 @@ __device__ __forceinline__ void fd_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
                     xh ^= SH[m | (1 << mb)];
                 }
             } else {
-                const uint32_t* p = Img<T, QL>::at(lds, c, k | (1u << b));
-                const uint32_t vl = p[0], vh = p[Img<T, QL>::PLANE];
-                const bool take = !((k >> b) & 1);
-                xl ^= take ? vl : 0u;
-                xh ^= take ? vh : 0u;
+                // bit sb of the row set s: above the lane-half bit it is a bit
+                // of the (uniform) wave index, and a term not taken is skipped
+                constexpr int LOG_HWS = Geo<T>::HWS == 2 ? 1 : 0;
+                const int sb = LB ? b : b - R;
+                if (sb >= LOG_HWS) {
+                    if (!((c.w >> (sb - LOG_HWS)) & 1)) {
+                        const uint32_t* p = Img<T, QL>::at(lds, c, k | (1u << b));
+                        xl ^= p[0];
+                        xh ^= p[Img<T, QL>::PLANE];
+                    }
+                } else {
+                    const uint32_t* p = Img<T, QL>::at(lds, c, k | (1u << b));
+                    const uint32_t vl = p[0], vh = p[Img<T, QL>::PLANE];
+                    const bool take = !((k >> b) & 1);
+                    xl ^= take ? vl : 0u;
+                    xh ^= take ? vh : 0u;
+                }
             }
         }
         L[m] = xl;
