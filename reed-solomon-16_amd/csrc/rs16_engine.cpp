@@ -177,7 +177,12 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* 
         RS16_PASS(ENC_SINGLE, L, a, 1, s);
         return RS16_OK;
     }
-    const int lo = L / 2, hi = L - lo;
+#ifndef RS16_ENC_LO_UP
+#define RS16_ENC_LO_UP 0
+#endif
+    // odd L: the extra row bit goes to the strided two-direction pass (0) or
+    // to the contiguous first / last passes (1)
+    const int lo = (L + RS16_ENC_LO_UP) / 2, hi = L - lo;
     a.out = Z;
     a.lo = 0;
     RS16_PASS(ENC_FIRST, lo, a, 1u << hi, s);

@@ -72,10 +72,16 @@ RS16_PROG(DEC_LAST, LD_DEC_LAST, false, false, true, ST_RESTORE)
 RS16_PROG(DEC_SINGLE, LD_GATHER_DEC, true, true, true, ST_RESTORE)
 #undef RS16_PROG
 
+// Quads per tile row for T > 4 (32: a wave holds two 16-row sets of 32
+// quads; 16: four row sets of 16 quads, half-size workgroups).
+#ifndef RS16_QW
+#define RS16_QW 32
+#endif
 template <int T> struct Geo {
     static constexpr int R = T > 4 ? 4 : T;               // row bits held in registers
     static constexpr int NR = 1 << R;                     // rows per thread (a row set)
-    static constexpr int Q = T > 4 ? 32 : 64;             // quads per tile row
+    // quads per tile row (a workgroup needs SETS >= HWS: RS16_QW < 32 from T = 6)
+    static constexpr int Q = T > 5 ? RS16_QW : (T > 4 ? 32 : 64);
     static constexpr int HWS = 64 / Q;                    // row sets per wave
     static constexpr int SETS = 1 << (T - R);             // row sets per tile
     static constexpr int W = SETS / HWS > 0 ? SETS / HWS : 1;  // waves per workgroup
@@ -491,7 +497,7 @@ __device__ __forceinline__ void fd_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
             } else {
                 // bit sb of the row set s: above the lane-half bit it is a bit
                 // of the (uniform) wave index, and a term not taken is skipped
-                constexpr int LOG_HWS = Geo<T>::HWS == 2 ? 1 : 0;
+                constexpr int LOG_HWS = Geo<T>::HWS == 4 ? 2 : (Geo<T>::HWS == 2 ? 1 : 0);
                 const int sb = LB ? b : b - R;
                 if (sb >= LOG_HWS) {
                     if (!((c.w >> (sb - LOG_HWS)) & 1)) {
