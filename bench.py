@@ -295,6 +295,29 @@ def main():
                                    "decode_gib_s": world * (k2 + m2) * S * n2 / td / GIB,
                                    "encode_us": te / n2 * 1e6, "decode_us": td / n2 * 1e6}
 
+    if not args.no_extra and loss >= 100:
+        # 1 % loss (benches/benchmarks.rs:84-87): originals 0..k-L and
+        # recovery 0..L received, L = min(k, m) / 100; the last L originals
+        # are restored in place.
+        L1 = loss // 100
+        of1 = np.ones(k, np.uint8)
+        of1[k - L1:] = 0
+        rf1 = np.zeros(m, np.uint8)
+        rf1[:L1] = 1
+        d_of1, d_rf1 = DeviceArray.from_numpy(eng, of1), DeviceArray.from_numpy(eng, rf1)
+        o1 = original.copy()
+        o1[k - L1:] = 0  # lost: must come back from the decode
+        d_r1 = DeviceArray.from_numpy(eng, o1)
+        d1 = lambda: rs16.decode_device(k, m, S, d_r1.ptr, d_of1.ptr, d_rec.ptr, d_rf1.ptr, k - L1, L1, engine=eng)
+        d1()
+        assert np.array_equal(d_r1.download(shape=(k, S)), original), "1 % loss decode did not restore"
+        for _ in range(args.warmup):
+            d1()
+        t1 = timed(d1, args.steps)
+        extra["decode_1pct_loss"] = {"decode_gib_s": world * (k + m) * S * args.steps / t1 / GIB,
+                                     "decode_us": t1 / args.steps * 1e6, "lost_originals": L1,
+                                     "received": f"originals 0..{k - L1}, recovery 0..{L1}"}
+
     if not args.no_extra:
         # Shards that start and end in host memory (north_star: recorded beside
         # the device-resident rate): rs16_encode_host / rs16_decode_host on

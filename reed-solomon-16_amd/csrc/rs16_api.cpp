@@ -698,7 +698,7 @@ extern "C" void* rs16_device_alloc(rs16_engine* e, size_t bytes, rs16_error* err
     return p;
 }
 extern "C" void rs16_device_free(rs16_engine* e, void* p) {
-    if (!p) return;
+    if (!e || !p) return;
     (void)hipSetDevice(e->device);
     (void)hipFree(p);
 }
@@ -711,7 +711,7 @@ extern "C" void* rs16_host_alloc(rs16_engine* e, size_t bytes, rs16_error* err) 
     return p;
 }
 extern "C" void rs16_host_free(rs16_engine* e, void* p) {
-    if (!p) return;
+    if (!e || !p) return;
     (void)hipSetDevice(e->device);
     (void)hipHostFree(p);
 }

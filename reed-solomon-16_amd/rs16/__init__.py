@@ -14,7 +14,9 @@ There is no CPU fallback.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
+import weakref
 from typing import Iterable, Iterator, Optional, Tuple
 
 import numpy as np
@@ -147,6 +149,7 @@ class Engine:
         if not self.h:
             raise Error._from_c(self._err)
         self.device = device
+        _live_engines.add(self)
 
     def close(self):
         if getattr(self, "h", None):
@@ -229,6 +232,17 @@ class Engine:
 
 
 _default_engines = {}
+_live_engines = weakref.WeakSet()
+
+
+@atexit.register
+def _close_engines():
+    # Close engines while the HIP runtime is still up, in a defined order
+    # (module globals are torn down in arbitrary order at interpreter exit);
+    # device arrays still alive after this see engine.h None and are left
+    # to the runtime.
+    for e in list(_live_engines):
+        e.close()
 
 
 def default_engine(device: Optional[int] = None) -> Engine:

@@ -42,7 +42,7 @@ class DeviceArray:
 
     def __del__(self):
         try:
-            if self.ptr:
+            if self.ptr and self.engine.h:  # engine closed first (interpreter exit): leave it to the runtime
                 lib().rs16_device_free(self.engine.h, self.ptr)
         except Exception:
             pass
@@ -73,7 +73,7 @@ class PinnedArray:
 
     def __del__(self):
         try:
-            if self.ptr:
+            if self.ptr and self.engine.h:
                 self.array = None
                 lib().rs16_host_free(self.engine.h, self.ptr)
         except Exception:

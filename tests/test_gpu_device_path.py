@@ -170,3 +170,20 @@ def test_rate_decoder_zero_tiles():
         assert set(restored) == set(np.flatnonzero(~om).tolist())
         for i, v in restored.items():
             assert v == original[i].tobytes(), i
+
+
+def test_configs4_per_gpu_column_slice(eng):
+    # BASELINE configs[4]: 32768:32768 x 64 KiB over 8 GPUs = 8 KiB of every
+    # shard per GPU (rs16/columns.py).  Full-size parity by column
+    # independence: two 1 KiB column slices of the 8 KiB device encode equal
+    # the oracle's encode of those slices alone; 100 % loss decode restores all.
+    k = m = 32768
+    sb = 64 * 1024 // 8
+    original = np.random.default_rng(4).integers(0, 256, (k, sb), dtype=np.uint8)
+    recovery = dev_encode(eng, original, m)
+    for c0 in (0, sb - 1024):
+        want = O.encode(k, m, np.ascontiguousarray(original[:, c0:c0 + 1024]))
+        assert np.array_equal(recovery[:, c0:c0 + 1024], want), c0
+    om = np.zeros(k, bool)
+    rm = np.ones(m, bool)
+    assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
