@@ -1,5 +1,6 @@
 // rs16_engine.cpp -- engine object: tables in HBM, engine-level transforms
 // as HBM passes, and the fused encode/decode pass sequences.
+#include <cstdlib>
 #include "rs16_engine.hpp"
 
 #include <algorithm>
@@ -214,7 +215,16 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_
     return decode_passes(g, S, seg_a, flags_a, seg_b, flags_b, rest, Z, U, (uint8_t*)ws_zflag.p, s, err);
 }
 
-// Erasure logs e = eval_poly(erasure vector) into ws_elog (3 small kernels).
+// RS16_EVAL_FULL=1 (diagnostic): always the 3-kernel 65536-point eval_poly.
+static bool eval_full_forced() {
+    static const bool f = [] {
+        const char* v = std::getenv("RS16_EVAL_FULL");
+        return v && v[0] == '1';
+    }();
+    return f;
+}
+
+// Erasure logs e = eval_poly(erasure vector) into ws_elog (2-3 small kernels).
 int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
                              rs16_error* err) {
     RS16_HIP(ws_work32.reserve(GF_ORDER * 4));
@@ -232,8 +242,14 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // 65536-row decodes run their first and last passes on 256-row tiles,
     // which finish eval_poly's last 256-point FWHT themselves.
     elog_fused = ilog2(g.n) == 16;
-    RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s,
-                                         !elog_fused));
+    if (g.high && g.n <= 2048 && !eval_full_forced()) {
+        // erasures are zero from row n on: only n/256 live blocks (rs16_misc.hip)
+        RS16_HIP(launch_eval_poly_small(es, (uint32_t)g.n, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh,
+                                        s));
+    } else {
+        RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s,
+                                             !elog_fused));
+    }
     return prof_end(NUM_PROGS, s, ev, err);
 }
 

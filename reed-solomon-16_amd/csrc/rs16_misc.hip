@@ -173,6 +173,78 @@ hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uin
                            nullptr);
     return hipGetLastError();
 }
+// eval_poly of a high-rate decode with n <= 2048 work rows:
+// the erasure vector is zero from row n on (rate_high.rs:183-197, the
+// truncation of the first fwht), so with H = H_lo H_hi only the NB = n/256
+// blocks of row bits 8-15 below n carry input, and only rows < n of the
+// output are consumed.  One workgroup per low index j (row bits 0-7):
+//   x[h']  = sum_i (-1)^|j&i| e[256h' + i]          (H_lo of the NB live blocks)
+//   w[h]   = LW[256h + j] * sum_h' (-1)^|h&h'| x[h'] (H_hi, x LogWalsh)
+//   z[h''] = sum_h (-1)^|h''&h| w[h],   h'' < NB     (H_hi, live outputs only)
+// as integer sums (|sum| < 2^24) reduced mod 65535 once; the last H_lo over the
+// NB output blocks is fwht_lo_kernel.  Same residues as the 3-kernel path.
+template <int NB> __device__ __forceinline__ void block_sum(int (&v)[NB], int (*sh)[4]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+        if (lane == 0) sh[k][w] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NB; k++) v[k] = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
+    __syncthreads();
+}
+__device__ __forceinline__ uint32_t mod65535(int v) {
+    const int r = v % 65535;
+    return (uint32_t)(r < 0 ? r + 65535 : r);
+}
+template <int NB>
+__global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const uint16_t* log_walsh, uint32_t* z) {
+    __shared__ int sh[NB][4];
+    const uint32_t j = blockIdx.x, t = threadIdx.x;
+    int v[NB];
+    const bool neg1 = __builtin_popcount(j & t) & 1;
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int x = (int)erasure_at(e, (uint32_t)h * 256u + t);
+        v[h] = neg1 ? -x : x;
+    }
+    block_sum<NB>(v, sh);
+    int y = 0;
+#pragma unroll
+    for (int h = 0; h < NB; h++) {
+        const int x = (int)mod65535(v[h]);
+        y += (__builtin_popcount(t & (uint32_t)h) & 1) ? -x : x;
+    }
+    const int w = (int)(((uint64_t)mod65535(y) * log_walsh[t * 256u + j]) % GF_MODULUS);
+#pragma unroll
+    for (int h = 0; h < NB; h++) v[h] = (__builtin_popcount(t & (uint32_t)h) & 1) ? -w : w;
+    block_sum<NB>(v, sh);
+    if (t < NB) {
+        int r = 0;
+#pragma unroll
+        for (int h = 0; h < NB; h++)
+            if ((uint32_t)h == t) r = v[h];
+        z[t * 256u + j] = mod65535(r);
+    }
+}
+
+hipError_t launch_eval_poly_small(const ErasureSpec& e, uint32_t n, uint32_t* work, uint32_t* out_elog,
+                                  const uint16_t* log_walsh, hipStream_t s) {
+    const uint32_t nb = n <= 256 ? 1 : n / 256;
+    switch (nb) {
+        case 1: hipLaunchKernelGGL(eval_small_kernel<1>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
+        case 2: hipLaunchKernelGGL(eval_small_kernel<2>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
+        case 4: hipLaunchKernelGGL(eval_small_kernel<4>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
+        case 8: hipLaunchKernelGGL(eval_small_kernel<8>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
+        default: return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(nb), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
+                       nullptr);
+    return hipGetLastError();
+}
 hipError_t launch_eval_poly_u16(uint16_t* data, uint32_t* work, const uint16_t* log_walsh, hipStream_t s) {
     ErasureSpec e{};
     hipLaunchKernelGGL((fwht_hi_kernel<2, 0>), dim3(256), dim3(256), 0, s, e, nullptr, data, work, nullptr);
