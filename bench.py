@@ -174,7 +174,9 @@ def main():
     from rs16.util import generate_original
 
     k, m, S = args.original, args.recovery, args.shard_bytes
-    eng = rs16.Engine(local)
+    # RS16_BENCH_SHARE_GPU=1: every rank on GPU 0 (rehearsal of the N > 1
+    # path on a one-GPU box only; the driver's N-GPU runs use one GPU per rank)
+    eng = rs16.Engine(0 if os.environ.get("RS16_BENCH_SHARE_GPU") == "1" else local)
     seed = rank & 0xFF
     original = generate_original(k, S, seed)
     d_orig = DeviceArray.from_numpy(eng, original)
