@@ -18,7 +18,17 @@
  *    device; `stream` is a hipStream_t (NULL = the engine's own stream).
  *    Device-pointer calls are asynchronous on that stream.
  *  - One engine must not be used from two threads at once (it owns scratch
- *    workspace); create one engine per device/thread.
+ *    workspace); create one engine per device/thread.  It may be used on
+ *    several streams: a call that needs the engine's scratch on stream s
+ *    first makes s wait (hipStreamWaitEvent) for the engine's previous such
+ *    call when that was issued on another stream, so two streams never
+ *    share the scratch concurrently (calls on one engine serialise; use one
+ *    engine per stream for concurrent codecs).
+ *  - rs16_engine_free synchronises the device, releases the work space of
+ *    every encoder/decoder created on the engine and detaches them: a
+ *    detached encoder/decoder fails every call with RS16_INVALID_ARGUMENT,
+ *    and rs16_{en,de}coder_free of it only frees its host memory (safe in
+ *    any order at process exit).
  */
 #ifndef RS16_H
 #define RS16_H
@@ -85,9 +95,14 @@ int rs16_engine_ifft(rs16_engine* eng, void* data, size_t shard_count, size_t sh
 int rs16_engine_ifft_skew_end(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, size_t pos,
                               size_t size, size_t truncated_size, void* stream, rs16_error* err);
 /* Engine::fwht (src/engine.rs:175) on a device u16[65536]; data beyond
- * truncated_size must be zero (the only way eval_poly uses it). */
+ * truncated_size must be zero (the only way eval_poly uses it).  The
+ * butterflies are exact in Z/65535 (ones' complement): an output equals the
+ * reference's as a residue, and may read 65535 where the reference has 0 or
+ * the reverse (both mean the same log, exp[65535] == exp[0],
+ * src/engine/tables.rs:118). */
 int rs16_engine_fwht(rs16_engine* eng, uint16_t* d_data, size_t truncated_size, void* stream, rs16_error* err);
-/* Engine::eval_poly (src/engine.rs:207-218) on a device u16[65536]. */
+/* Engine::eval_poly (src/engine.rs:207-218) on a device u16[65536]; same
+ * residue convention as rs16_engine_fwht. */
 int rs16_engine_eval_poly(rs16_engine* eng, uint16_t* d_erasures, size_t truncated_size, void* stream,
                           rs16_error* err);
 /* Engine::mul (src/engine.rs:198): x[] *= log_m, bytes % 64 == 0. */
@@ -128,7 +143,11 @@ int rs16_encoder_add_original_shard(rs16_encoder* enc, const void* shard, size_t
 /* same, shard in device memory (copied on the engine stream). */
 int rs16_encoder_add_original_shard_device(rs16_encoder* enc, const void* d_shard, size_t len, rs16_error* err);
 /* encode (rate_high.rs:44-83 / rate_low.rs:44-83); on success the
- * EncoderResult (src/encoder_result.rs) is valid until rs16_encoder_result_drop. */
+ * EncoderResult (src/encoder_result.rs) is valid until rs16_encoder_result_drop.
+ * The encode works in place: calling it again while the result is held
+ * returns RS16_INVALID_ARGUMENT (the reference's &mut borrow makes that a
+ * compile error, src/rate.rs:157-166); add_original_shard in that state
+ * returns TooManyOriginalShards, as every original is in. */
 int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err);
 /* EncoderResult::recovery (src/encoder_result.rs:16-19): device pointer, NULL if index >= recovery_count. */
 const void* rs16_encoder_recovery_device(rs16_encoder* enc, size_t index);
@@ -153,7 +172,9 @@ int rs16_decoder_add_original_shard_device(rs16_decoder* dec, size_t index, cons
                                            rs16_error* err);
 int rs16_decoder_add_recovery_shard_device(rs16_decoder* dec, size_t index, const void* d_shard, size_t len,
                                            rs16_error* err);
-/* decode (rate_high.rs:168-247 / rate_low.rs:168-247); DecoderResult valid until drop. */
+/* decode (rate_high.rs:168-247 / rate_low.rs:168-247); DecoderResult valid until drop.
+ * The decode restores in place: decode or add_*_shard while the result is
+ * held returns RS16_INVALID_ARGUMENT (a compile error in the reference). */
 int rs16_decoder_decode(rs16_decoder* dec, rs16_error* err);
 /* DecoderResult::restored_original (src/decoder_result.rs:16-19): device pointer or NULL. */
 const void* rs16_decoder_restored_original_device(rs16_decoder* dec, size_t index);
@@ -173,8 +194,12 @@ int rs16_encode_device(rs16_engine* eng, size_t original_count, size_t recovery_
  * holds original_count shard slots (received ones valid, flagged by the
  * device byte array d_original_received); d_recovery holds recovery_count
  * slots flagged by d_recovery_received.  The host passes the number of
- * received shards of each kind (for the reference's NotEnoughShards /
- * nothing-to-do checks).  Lost originals are restored in place into
+ * received shards of each kind: they give the reference's NotEnoughShards /
+ * nothing-to-do checks AND select the launch -- a count of 0 means "no
+ * shard of this kind was received", and the first pass then launches no
+ * tile of that segment.  The counts MUST equal the number of nonzero flags
+ * (a 0 count with set flags drops those shards and restores wrong data
+ * without an error).  Lost originals are restored in place into
  * d_original.  Default rate selection as ReedSolomonDecoder. */
 int rs16_decode_device(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
                        void* d_original, const uint8_t* d_original_received, const void* d_recovery,
@@ -204,6 +229,10 @@ void rs16_device_free(rs16_engine* eng, void* d_ptr);
 int rs16_memcpy_htod(rs16_engine* eng, void* d_dst, const void* src, size_t bytes, void* stream, rs16_error* err);
 int rs16_memcpy_dtoh(rs16_engine* eng, void* dst, const void* d_src, size_t bytes, void* stream, rs16_error* err);
 int rs16_memset_device(rs16_engine* eng, void* d_dst, int value, size_t bytes, void* stream, rs16_error* err);
+/* Streams (hipStream_t, non-blocking) on the engine's device, for callers
+ * without HIP headers that run codecs on streams of their own. */
+void* rs16_stream_create(rs16_engine* eng, rs16_error* err);
+void rs16_stream_destroy(rs16_engine* eng, void* stream);
 /* Page-locked host staging memory (hipHostMalloc): shards that start and end
  * in host memory move over PCIe at DMA rate from/to these buffers (the
  * host-resident path of EncoderWork / DecoderWork, src/rate/encoder_work.rs:49-69). */

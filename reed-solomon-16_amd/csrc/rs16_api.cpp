@@ -164,6 +164,9 @@ static int resolve_rate(int rate, size_t k, size_t m, size_t S, bool* high, rs16
 // ---------------------------------------------------------------------------
 // Engine.
 // ---------------------------------------------------------------------------
+static void detach(rs16_encoder* enc);
+static void detach(rs16_decoder* dec);
+
 extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
     int ndev = 0;
     hipError_t he = hipGetDeviceCount(&ndev);
@@ -193,7 +196,9 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
 extern "C" void rs16_engine_free(rs16_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    (void)hipDeviceSynchronize();  // every stream that used the engine's scratch or its children's work
+    for (rs16_encoder* c : e->encoders) detach(c);
+    for (rs16_decoder* c : e->decoders) detach(c);
     e->ws_z.release();
     e->ws_u.release();
     e->ws_fd.release();
@@ -207,6 +212,7 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     }
     e->hflags.release();
     if (e->hev) (void)hipEventDestroy(e->hev);
+    if (e->order_ev) (void)hipEventDestroy(e->order_ev);
     if (e->d_skew_entry) (void)hipFree(e->d_skew_entry);
     if (e->d_mul_tab) (void)hipFree(e->d_mul_tab);
     if (e->d_log_walsh) (void)hipFree(e->d_log_walsh);
@@ -259,6 +265,7 @@ extern "C" int rs16_engine_ifft_skew_end(rs16_engine* e, void* data, size_t shar
 extern "C" int rs16_engine_fwht(rs16_engine* e, uint16_t* d, size_t trunc, void* stream, rs16_error* err) {
     if (trunc > GF_ORDER) return set_error(err, RS16_INVALID_ARGUMENT);
     if (int rc = e->activate(err)) return rc;
+    if (int rc = e->order(e->pick(stream), err)) return rc;
     RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
     RS16_HIP(launch_fwht_u16(d, (uint32_t*)e->ws_work32.p, e->pick(stream)));
     return set_error(err, RS16_OK);
@@ -266,6 +273,7 @@ extern "C" int rs16_engine_fwht(rs16_engine* e, uint16_t* d, size_t trunc, void*
 extern "C" int rs16_engine_eval_poly(rs16_engine* e, uint16_t* d, size_t trunc, void* stream, rs16_error* err) {
     if (trunc > GF_ORDER) return set_error(err, RS16_INVALID_ARGUMENT);
     if (int rc = e->activate(err)) return rc;
+    if (int rc = e->order(e->pick(stream), err)) return rc;
     RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
     RS16_HIP(launch_eval_poly_u16(d, (uint32_t*)e->ws_work32.p, e->d_log_walsh, e->pick(stream)));
     return set_error(err, RS16_OK);
@@ -294,6 +302,7 @@ extern "C" int rs16_engine_formal_derivative(rs16_engine* e, void* data, size_t 
     if ((S & 63) || S == 0 || !is_pow2(n)) return set_error(err, RS16_INVALID_ARGUMENT);
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
     RS16_HIP(e->ws_fd.reserve(n * S));
     RS16_HIP(launch_formal_derivative((uint8_t*)e->ws_fd.p, (const uint8_t*)data, n, S, s));
     RS16_HIP(hipMemcpyAsync(data, e->ws_fd.p, n * S, hipMemcpyDeviceToDevice, s));
@@ -304,14 +313,26 @@ extern "C" int rs16_engine_formal_derivative(rs16_engine* e, void* data, size_t 
 // Encoder -- EncoderWork (src/rate/encoder_work.rs) + Rate encoders.
 // ---------------------------------------------------------------------------
 struct rs16_encoder {
-    rs16_engine* eng;
+    rs16_engine* eng;  // nullptr once the engine was freed (detached)
     int rate_kind;
     bool high = true;
+    // encoded: an EncoderResult is alive (encode ran, result not dropped).
+    // The encode works in place, so a second encode before the drop would
+    // read recovery rows as originals; the reference's borrow rules rule
+    // that out at compile time (src/rate.rs:157-166), here it is an error.
+    bool encoded = false;
     size_t k = 0, m = 0, S = 0, work_count = 0, received = 0;
     DevBuf work;
 };
 
+static void detach(rs16_encoder* enc) {
+    enc->work.release();
+    enc->eng = nullptr;
+}
+template <class V, class T> static void forget(V& v, T* x) { v.erase(std::remove(v.begin(), v.end(), x), v.end()); }
+
 static int encoder_reset_impl(rs16_encoder* enc, size_t k, size_t m, size_t S, rs16_error* err) {
+    if (!enc->eng) return set_error(err, RS16_INVALID_ARGUMENT);
     bool high;
     if (int rc = resolve_rate(enc->rate_kind, k, m, S, &high, err)) return rc;
     const size_t wc = rs16_encoder_work_count(high, k, m);
@@ -323,14 +344,17 @@ static int encoder_reset_impl(rs16_encoder* enc, size_t k, size_t m, size_t S, r
     enc->S = S;
     enc->work_count = wc;
     enc->received = 0;
+    enc->encoded = false;
     return set_error(err, RS16_OK);
 }
 
 extern "C" rs16_encoder* rs16_encoder_new(rs16_engine* eng, int rate, size_t k, size_t m, size_t S, rs16_error* err) {
+    if (!eng) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
     rs16_encoder* enc = new (std::nothrow) rs16_encoder();
     if (!enc) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
     enc->eng = eng;
     enc->rate_kind = rate;
+    eng->encoders.push_back(enc);
     if (encoder_reset_impl(enc, k, m, S, err)) {
         rs16_encoder_free(enc);
         return nullptr;
@@ -339,15 +363,19 @@ extern "C" rs16_encoder* rs16_encoder_new(rs16_engine* eng, int rate, size_t k, 
 }
 extern "C" void rs16_encoder_free(rs16_encoder* enc) {
     if (!enc) return;
-    (void)hipSetDevice(enc->eng->device);
-    (void)hipStreamSynchronize(enc->eng->stream);
-    enc->work.release();
+    if (rs16_engine* e = enc->eng) {
+        (void)hipSetDevice(e->device);
+        (void)hipStreamSynchronize(e->stream);
+        enc->work.release();
+        forget(e->encoders, enc);
+    }
     delete enc;
 }
 extern "C" int rs16_encoder_reset(rs16_encoder* enc, size_t k, size_t m, size_t S, rs16_error* err) {
     return encoder_reset_impl(enc, k, m, S, err);
 }
 static int encoder_add(rs16_encoder* enc, const void* shard, size_t len, bool device, rs16_error* err) {
+    if (!enc->eng) return set_error(err, RS16_INVALID_ARGUMENT);
     if (enc->received == enc->k) return set_error(err, RS16_TOO_MANY_ORIGINAL_SHARDS, enc->k);
     if (len != enc->S) return set_error(err, RS16_DIFFERENT_SHARD_SIZE, enc->S, len);
     if (int rc = enc->eng->activate(err)) return rc;
@@ -365,9 +393,11 @@ extern "C" int rs16_encoder_add_original_shard_device(rs16_encoder* enc, const v
     return encoder_add(enc, d, len, true, err);
 }
 extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
+    if (!enc->eng || enc->encoded) return set_error(err, RS16_INVALID_ARGUMENT);
     if (enc->received != enc->k) return set_error(err, RS16_TOO_FEW_ORIGINAL_SHARDS, enc->k, enc->received);
     rs16_engine* e = enc->eng;
     if (int rc = e->activate(err)) return rc;
+    if (int rc = e->order(e->stream, err)) return rc;
     uint8_t* w = (uint8_t*)enc->work.p;
     const size_t chunk = next_pow2(enc->m);
     int rc;
@@ -378,38 +408,54 @@ extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
     else
         rc = e->encode_low_generic(enc->k, enc->m, enc->S, w, enc->work_count, e->stream, err);
     if (rc) return rc;
+    enc->encoded = true;
     return set_error(err, RS16_OK);
 }
 extern "C" const void* rs16_encoder_recovery_device(rs16_encoder* enc, size_t index) {
-    return index < enc->m ? (const uint8_t*)enc->work.p + index * enc->S : nullptr;
+    return enc->eng && enc->encoded && index < enc->m ? (const uint8_t*)enc->work.p + index * enc->S : nullptr;
 }
 extern "C" int rs16_encoder_recovery_copy(rs16_encoder* enc, size_t index, void* dst, size_t len, rs16_error* err) {
     const void* src = rs16_encoder_recovery_device(enc, index);
     if (!src) return set_error(err, RS16_OK), 0;
     if (len < enc->S) return set_error(err, RS16_INVALID_ARGUMENT), -1;
-    if (enc->eng->activate(err)) return -1;
+    if (enc->eng->activate(err)) return -1;  // (src != nullptr: attached)
     hipError_t he = hipMemcpyAsync(dst, src, enc->S, hipMemcpyDeviceToHost, enc->eng->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(enc->eng->stream);
     if (he != hipSuccess) return hip_fail(err, he), -1;
     return set_error(err, RS16_OK), 1;
 }
-extern "C" void rs16_encoder_result_drop(rs16_encoder* enc) { enc->received = 0; }
+extern "C" void rs16_encoder_result_drop(rs16_encoder* enc) {
+    enc->received = 0;
+    enc->encoded = false;
+}
 extern "C" int rs16_encoder_is_high_rate(const rs16_encoder* enc) { return enc->high; }
 
 // ---------------------------------------------------------------------------
 // Decoder -- DecoderWork (src/rate/decoder_work.rs) + Rate decoders.
 // ---------------------------------------------------------------------------
 struct rs16_decoder {
-    rs16_engine* eng;
+    rs16_engine* eng;  // nullptr once the engine was freed (detached)
     int rate_kind;
     bool high = true;
+    // decoded: a DecoderResult is alive.  The decode restores in place, so
+    // adding shards or decoding again before the drop is an error (the
+    // reference's borrow rules, src/rate.rs:235-244).
+    bool decoded = false;
     size_t k = 0, m = 0, S = 0, work_count = 0;
     size_t orig_base = 0, rec_base = 0, orig_recv = 0, rec_recv = 0;
     std::vector<uint8_t> received;  // by work position
     DevBuf work, ubuf, flags;       // work = shards (z), ubuf = second work array (u)
 };
 
+static void detach(rs16_decoder* d) {
+    d->work.release();
+    d->ubuf.release();
+    d->flags.release();
+    d->eng = nullptr;
+}
+
 static int decoder_reset_impl(rs16_decoder* d, size_t k, size_t m, size_t S, rs16_error* err) {
+    if (!d->eng) return set_error(err, RS16_INVALID_ARGUMENT);
     bool high;
     if (int rc = resolve_rate(d->rate_kind, k, m, S, &high, err)) return rc;
     const size_t wc = rs16_decoder_work_count(high, k, m);
@@ -425,15 +471,18 @@ static int decoder_reset_impl(rs16_decoder* d, size_t k, size_t m, size_t S, rs1
     d->orig_base = high ? next_pow2(m) : 0;  // rate_high.rs:279-299 / rate_low.rs:279-299
     d->rec_base = high ? 0 : next_pow2(k);
     d->orig_recv = d->rec_recv = 0;
+    d->decoded = false;
     d->received.assign(std::max(d->received.size(), wc), 0);
     return set_error(err, RS16_OK);
 }
 
 extern "C" rs16_decoder* rs16_decoder_new(rs16_engine* eng, int rate, size_t k, size_t m, size_t S, rs16_error* err) {
+    if (!eng) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
     rs16_decoder* d = new (std::nothrow) rs16_decoder();
     if (!d) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
     d->eng = eng;
     d->rate_kind = rate;
+    eng->decoders.push_back(d);
     if (decoder_reset_impl(d, k, m, S, err)) {
         rs16_decoder_free(d);
         return nullptr;
@@ -442,11 +491,12 @@ extern "C" rs16_decoder* rs16_decoder_new(rs16_engine* eng, int rate, size_t k, 
 }
 extern "C" void rs16_decoder_free(rs16_decoder* d) {
     if (!d) return;
-    (void)hipSetDevice(d->eng->device);
-    (void)hipStreamSynchronize(d->eng->stream);
-    d->work.release();
-    d->ubuf.release();
-    d->flags.release();
+    if (rs16_engine* e = d->eng) {
+        (void)hipSetDevice(e->device);
+        (void)hipStreamSynchronize(e->stream);
+        detach(d);
+        forget(e->decoders, d);
+    }
     delete d;
 }
 extern "C" int rs16_decoder_reset(rs16_decoder* d, size_t k, size_t m, size_t S, rs16_error* err) {
@@ -454,6 +504,7 @@ extern "C" int rs16_decoder_reset(rs16_decoder* d, size_t k, size_t m, size_t S,
 }
 static int decoder_add(rs16_decoder* d, bool original, size_t index, const void* shard, size_t len, bool device,
                        rs16_error* err) {
+    if (!d->eng || d->decoded) return set_error(err, RS16_INVALID_ARGUMENT);
     const size_t count = original ? d->k : d->m;
     const size_t pos = (original ? d->orig_base : d->rec_base) + index;
     if (index >= count)
@@ -486,12 +537,14 @@ extern "C" int rs16_decoder_add_recovery_shard_device(rs16_decoder* d, size_t i,
     return decoder_add(d, false, i, s, len, true, err);
 }
 extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
+    if (!d->eng || d->decoded) return set_error(err, RS16_INVALID_ARGUMENT);
     // decode_begin (src/rate/decoder_work.rs:120-139)
     if (d->orig_recv + d->rec_recv < d->k)
         return set_error(err, RS16_NOT_ENOUGH_SHARDS, d->k, d->orig_recv, d->rec_recv);
-    if (d->orig_recv == d->k) return set_error(err, RS16_OK);  // nothing to do
+    if (d->orig_recv == d->k) return d->decoded = true, set_error(err, RS16_OK);  // nothing to do
     rs16_engine* e = d->eng;
     if (int rc = e->activate(err)) return rc;
+    if (int rc = e->order(e->stream, err)) return rc;
     DecodeGeom g = decode_geom(d->high, d->k, d->m);
     g.a_recv = d->high ? d->rec_recv : d->orig_recv;
     g.b_recv = d->high ? d->orig_recv : d->rec_recv;
@@ -504,11 +557,12 @@ extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
                                  w, (uint8_t*)d->ubuf.p, e->stream, err))
         return rc;
     RS16_HIP(hipStreamSynchronize(e->stream));  // host flag buffers are pageable
+    d->decoded = true;
     return set_error(err, RS16_OK);
 }
 extern "C" const void* rs16_decoder_restored_original_device(rs16_decoder* d, size_t index) {
     const size_t pos = d->orig_base + index;
-    if (index < d->k && !d->received[pos]) return (const uint8_t*)d->work.p + pos * d->S;
+    if (d->eng && d->decoded && index < d->k && !d->received[pos]) return (const uint8_t*)d->work.p + pos * d->S;
     return nullptr;
 }
 extern "C" int rs16_decoder_restored_original_copy(rs16_decoder* d, size_t index, void* dst, size_t len,
@@ -523,6 +577,7 @@ extern "C" int rs16_decoder_restored_original_copy(rs16_decoder* d, size_t index
     return set_error(err, RS16_OK), 1;
 }
 extern "C" void rs16_decoder_result_drop(rs16_decoder* d) {  // DecoderWork::reset_received
+    d->decoded = false;
     d->orig_recv = d->rec_recv = 0;
     std::fill(d->received.begin(), d->received.end(), 0);
 }
@@ -550,6 +605,7 @@ extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
     RS16_HIP(e->ws_z.reserve(rs16_encoder_work_count(high, k, m) * S));
     if (int rc = encode_dev(e, high, k, m, S, (const uint8_t*)d_original, (uint8_t*)d_recovery,
                             (uint8_t*)e->ws_z.p, s, err))
@@ -564,6 +620,7 @@ int rs16_engine::host_slots(rs16_error* err) {
     for (auto& sl : hslot)
         if (!sl.s) RS16_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
     if (!hev) RS16_HIP(hipEventCreateWithFlags(&hev, hipEventDisableTiming));
+    if (int rc = order(stream, err)) return rc;
     // start after the caller's earlier work on the engine stream
     RS16_HIP(hipEventRecord(hev, stream));
     for (auto& sl : hslot) RS16_HIP(hipStreamWaitEvent(sl.s, hev, 0));
@@ -630,6 +687,7 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
         RS16_HIP(sl.zflag.reserve(256));
     }
     // received flags -> device; erasure logs once, shared by every slice
+    if (int rc = e->order(e->stream, err)) return rc;
     RS16_HIP(e->hflags.reserve(k + m));
     uint8_t* d_of = (uint8_t*)e->hflags.p;
     uint8_t* d_rf = d_of + k;
@@ -671,6 +729,7 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     if (orig_recv == k) return set_error(err, RS16_OK);
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
     DecodeGeom g = decode_geom(high, k, m);
     g.a_recv = high ? rec_recv : orig_recv;
     g.b_recv = high ? orig_recv : rec_recv;
@@ -701,6 +760,21 @@ extern "C" void rs16_device_free(rs16_engine* e, void* p) {
     if (!e || !p) return;
     (void)hipSetDevice(e->device);
     (void)hipFree(p);
+}
+extern "C" void* rs16_stream_create(rs16_engine* e, rs16_error* err) {
+    if (e->activate(err)) return nullptr;
+    hipStream_t st = nullptr;
+    hipError_t he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (he != hipSuccess) return hip_fail(err, he), nullptr;
+    set_error(err, RS16_OK);
+    return (void*)st;
+}
+extern "C" void rs16_stream_destroy(rs16_engine* e, void* st) {
+    if (!e || !st) return;
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize((hipStream_t)st);
+    if (e->last_stream == (hipStream_t)st) e->last_stream = nullptr;
+    (void)hipStreamDestroy((hipStream_t)st);
 }
 extern "C" void* rs16_host_alloc(rs16_engine* e, size_t bytes, rs16_error* err) {
     if (e->activate(err)) return nullptr;

@@ -69,6 +69,16 @@ int rs16_engine::activate(rs16_error* err) {
     return RS16_OK;
 }
 
+int rs16_engine::order(hipStream_t s, rs16_error* err) {
+    if (last_stream && last_stream != s) {
+        if (!order_ev) RS16_HIP(hipEventCreateWithFlags(&order_ev, hipEventDisableTiming));
+        RS16_HIP(hipEventRecord(order_ev, last_stream));
+        RS16_HIP(hipStreamWaitEvent(s, order_ev, 0));
+    }
+    last_stream = s;
+    return RS16_OK;
+}
+
 int rs16_engine::prof_begin(hipStream_t s, hipEvent_t* ev, rs16_error* err) {
     *ev = nullptr;
     if (!profiling) return RS16_OK;

@@ -46,6 +46,9 @@ DecodeGeom decode_geom(bool high, size_t k, size_t m);
 
 }  // namespace rs16
 
+struct rs16_encoder;
+struct rs16_decoder;
+
 struct rs16_engine {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -71,6 +74,21 @@ struct rs16_engine {
 
     hipStream_t pick(void* s) const { return s ? (hipStream_t)s : stream; }
     int activate(rs16_error* err);
+
+    // The scratch buffers (ws_*) belong to the engine, not to a stream: a
+    // call that uses them on stream s first waits for the engine's previous
+    // such call when that ran on another stream (one event, recorded there),
+    // so calls on different streams cannot overwrite each other's scratch.
+    hipStream_t last_stream = nullptr;
+    hipEvent_t order_ev = nullptr;
+    int order(hipStream_t s, rs16_error* err);
+
+    // Encoders / decoders created on this engine.  rs16_engine_free releases
+    // their device work space and detaches them (eng = nullptr): a detached
+    // object answers every call with RS16_INVALID_ARGUMENT and
+    // rs16_{en,de}coder_free only frees its host memory.
+    std::vector<rs16_encoder*> encoders;
+    std::vector<rs16_decoder*> decoders;
 
     // Pass launch (with optional per-program hipEvent timing on the launch
     // stream; id NUM_PROGS = the eval_poly kernels of a decode).

@@ -245,17 +245,34 @@ hipError_t launch_eval_poly_small(const ErasureSpec& e, uint32_t n, uint32_t* wo
                        nullptr);
     return hipGetLastError();
 }
+// Engine-level fwht / eval_poly (the C ABI ops): the layers run in the
+// reference's order -- ascending distance, H_lo (bits 0-7) before H_hi
+// (bits 8-15) -- with its add_mod / sub_mod, so every output is the
+// reference's u16 bit for bit (NoSimd's radix-4 fwht_4 is two plain layers,
+// src/engine/engine_nosimd.rs:135-150; Naive, engine_naive.rs:75-92), not
+// only the same residue.  The log_walsh product is canonical (% 65535).
+template <bool MULW>
+__global__ void __launch_bounds__(256) fwht_hi_exact_kernel(const uint32_t* in32, uint32_t* out32, uint16_t* out16,
+                                                            const uint16_t* log_walsh) {
+    __shared__ uint32_t s[256];
+    const uint32_t idx = blockIdx.x + 256u * threadIdx.x;
+    s[threadIdx.x] = in32[idx];
+    fwht256_lds(s);
+    uint32_t v = s[threadIdx.x];
+    if (MULW) v = (uint32_t)(((uint64_t)v * log_walsh[idx]) % GF_MODULUS);
+    if (out16) out16[idx] = (uint16_t)v;
+    else out32[idx] = v;
+}
 hipError_t launch_eval_poly_u16(uint16_t* data, uint32_t* work, const uint16_t* log_walsh, hipStream_t s) {
-    ErasureSpec e{};
-    hipLaunchKernelGGL((fwht_hi_kernel<2, 0>), dim3(256), dim3(256), 0, s, e, nullptr, data, work, nullptr);
-    hipLaunchKernelGGL((fwht_lo_kernel<true, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, work, nullptr, log_walsh);
-    hipLaunchKernelGGL((fwht_hi_kernel<0, 1>), dim3(256), dim3(256), 0, s, e, work, nullptr, nullptr, data);
+    hipLaunchKernelGGL((fwht_lo_kernel<false, 1, 0>), dim3(256), dim3(256), 0, s, nullptr, data, work, nullptr, nullptr);
+    hipLaunchKernelGGL(fwht_hi_exact_kernel<true>, dim3(256), dim3(256), 0, s, work, work, nullptr, log_walsh);
+    hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, work, nullptr, nullptr);
+    hipLaunchKernelGGL(fwht_hi_exact_kernel<false>, dim3(256), dim3(256), 0, s, work, nullptr, data, nullptr);
     return hipGetLastError();
 }
 hipError_t launch_fwht_u16(uint16_t* data, uint32_t* work, hipStream_t s) {
-    ErasureSpec e{};
-    hipLaunchKernelGGL((fwht_hi_kernel<2, 0>), dim3(256), dim3(256), 0, s, e, nullptr, data, work, nullptr);
-    hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 1>), dim3(256), dim3(256), 0, s, work, nullptr, nullptr, data, nullptr);
+    hipLaunchKernelGGL((fwht_lo_kernel<false, 1, 0>), dim3(256), dim3(256), 0, s, nullptr, data, work, nullptr, nullptr);
+    hipLaunchKernelGGL(fwht_hi_exact_kernel<false>, dim3(256), dim3(256), 0, s, work, nullptr, data, nullptr);
     return hipGetLastError();
 }
 

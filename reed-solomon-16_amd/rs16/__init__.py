@@ -169,6 +169,17 @@ class Engine:
     def synchronize(self, stream=None):
         _check(lib().rs16_engine_synchronize(self.h, stream, C.byref(self._err)), self._err)
 
+    def create_stream(self) -> int:
+        """A new non-blocking hipStream_t on this engine's device (raw handle)."""
+        p = lib().rs16_stream_create(self.h, C.byref(self._err))
+        if not p:
+            raise Error._from_c(self._err)
+        return p
+
+    def destroy_stream(self, stream: int):
+        if self.h and stream:
+            lib().rs16_stream_destroy(self.h, stream)
+
     # per-pass hipEvent timing (include/rs16.h "Diagnostics")
     def set_profiling(self, enable: bool):
         _check(lib().rs16_engine_set_profiling(self.h, int(enable), C.byref(self._err)), self._err)
@@ -389,9 +400,14 @@ class RateEncoder:
         self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().rs16_encoder_free(self.h)
-            self.h = None
+        # Safe after the engine is gone: rs16_engine_free detaches its
+        # encoders, and freeing a detached one only frees host memory.
+        try:
+            if getattr(self, "h", None):
+                lib().rs16_encoder_free(self.h)
+                self.h = None
+        except Exception:
+            pass
 
     @staticmethod
     def supports(original_count, recovery_count) -> bool:
@@ -433,9 +449,12 @@ class RateDecoder:
         self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().rs16_decoder_free(self.h)
-            self.h = None
+        try:
+            if getattr(self, "h", None):
+                lib().rs16_decoder_free(self.h)
+                self.h = None
+        except Exception:
+            pass
 
     @staticmethod
     def supports(original_count, recovery_count) -> bool:

@@ -83,6 +83,8 @@ SIGNATURES = {
     "rs16_encode_host": (_i, [_p, _sz, _sz, _sz, _p, _p, _sz, _e]),
     "rs16_decode_host": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _p, _sz, _e]),
     "rs16_host_alloc": (_p, [_p, _sz, _e]),
+    "rs16_stream_create": (_p, [_p, _e]),
+    "rs16_stream_destroy": (None, [_p, _p]),
     "rs16_host_free": (None, [_p, _p]),
 }
 

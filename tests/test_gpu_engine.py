@@ -114,14 +114,10 @@ def test_formal_derivative(eng, n):
     assert np.array_equal(d.download(shape=x.shape), want)
 
 
-def residues(v):
-    v = v.astype(np.uint32)
-    v[v == 65535] = 0
-    return v
-
-
 @pytest.mark.parametrize("trunc", [65536, 2024, 3])
 def test_fwht_and_eval_poly(eng, trunc):
+    # bit-exact u16 outputs (not only residues mod 65535): the engine-level
+    # ops run the reference's layer order with its add_mod / sub_mod
     rng = np.random.default_rng(trunc)
     e = np.zeros(65536, np.uint16)
     e[:trunc] = rng.integers(0, 2, trunc)
@@ -129,12 +125,25 @@ def test_fwht_and_eval_poly(eng, trunc):
     eng.fwht(d.ptr, trunc)
     want = e.copy()
     O.fwht(want, trunc)
-    assert np.array_equal(residues(d.download(np.uint16)), residues(want))
+    assert np.array_equal(d.download(np.uint16), want)
     d.upload(e)
     eng.eval_poly(d.ptr, trunc)
     want = e.copy()
     O.eval_poly(want, trunc)
-    assert np.array_equal(residues(d.download(np.uint16)), residues(want))
+    assert np.array_equal(d.download(np.uint16), want)
+
+
+def test_fwht_full_range_values(eng):
+    # arbitrary u16 inputs (65535 included) -- exercises every add_mod /
+    # sub_mod wrap, where 0 and 65535 outputs differ bit-wise
+    rng = np.random.default_rng(5)
+    e = rng.integers(0, 65536, 65536, dtype=np.uint32).astype(np.uint16)
+    e[:64] = 65535
+    d = DeviceArray.from_numpy(eng, e)
+    eng.fwht(d.ptr, 65536)
+    want = e.copy()
+    O.fwht(want, 65536)
+    assert np.array_equal(d.download(np.uint16), want)
 
 
 def test_invalid_arguments(eng):
