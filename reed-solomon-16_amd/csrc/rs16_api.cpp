@@ -186,6 +186,8 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
     if ((he = hipMalloc(&e->d_skew_entry, t.skew_entry.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_mul_tab, t.mul_tab.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_log_walsh, GF_ORDER * 2)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_zero_sink, RS16_ZERO_BYTES + RS16_SINK_BYTES)) != hipSuccess) return fail(he);
+    if ((he = hipMemset(e->d_zero_sink, 0, RS16_ZERO_BYTES)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_skew_entry, t.skew_entry.data(), t.skew_entry.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_mul_tab, t.mul_tab.data(), t.mul_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_log_walsh, t.log_walsh.data(), GF_ORDER * 2, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
@@ -206,9 +208,10 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->ws_elog.release();
     e->ws_flags.release();
     e->ws_zflag.release();
+    e->ws_rbits.release();
     for (auto& sl : e->hslot) {
         if (sl.s) (void)hipStreamSynchronize(sl.s), (void)hipStreamDestroy(sl.s);
-        sl.orig.release(), sl.rec.release(), sl.z.release(), sl.u.release(), sl.zflag.release();
+        sl.orig.release(), sl.rec.release(), sl.z.release(), sl.u.release();
     }
     e->hflags.release();
     if (e->hev) (void)hipEventDestroy(e->hev);
@@ -216,6 +219,7 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     if (e->d_skew_entry) (void)hipFree(e->d_skew_entry);
     if (e->d_mul_tab) (void)hipFree(e->d_mul_tab);
     if (e->d_log_walsh) (void)hipFree(e->d_log_walsh);
+    if (e->d_zero_sink) (void)hipFree(e->d_zero_sink);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -684,7 +688,6 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
         RS16_HIP(sl.rec.reserve(m * W));
         RS16_HIP(sl.z.reserve((size_t)g.n * W));
         RS16_HIP(sl.u.reserve((size_t)g.n * W));
-        RS16_HIP(sl.zflag.reserve(256));
     }
     // received flags -> device; erasure logs once, shared by every slice
     if (int rc = e->order(e->stream, err)) return rc;
@@ -709,7 +712,7 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
         const uint8_t* o = (const uint8_t*)sl.orig.p;
         const uint8_t* r = (const uint8_t*)sl.rec.p;
         if (int rc = e->decode_passes(g, w, high ? r : o, fa, high ? o : r, fb, (uint8_t*)sl.orig.p,
-                                      (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, (uint8_t*)sl.zflag.p, sl.s, err))
+                                      (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, sl.s, err))
             return rc;
         // restored originals land in place; received rows come back unchanged
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_original + off, S, sl.orig.p, w, w, k, hipMemcpyDeviceToHost, sl.s));

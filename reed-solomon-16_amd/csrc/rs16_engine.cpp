@@ -55,6 +55,8 @@ static PassArgs base_args(const rs16_engine* e, size_t S) {
     std::memset(&a, 0, sizeof a);
     a.skew_entry = e->d_skew_entry;
     a.mul_tab = e->d_mul_tab;
+    a.zero = e->d_zero_sink;
+    a.sink = e->d_zero_sink + RS16_ZERO_BYTES;
     a.S = S;
     a.qrow = (uint32_t)(S / 8);
     return a;
@@ -221,8 +223,7 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_
                               const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                               hipStream_t s, rs16_error* err) {
     if (int rc = decode_eval(g, flags_a, flags_b, s, err)) return rc;
-    RS16_HIP(ws_zflag.reserve(256));
-    return decode_passes(g, S, seg_a, flags_a, seg_b, flags_b, rest, Z, U, (uint8_t*)ws_zflag.p, s, err);
+    return decode_passes(g, S, seg_a, flags_a, seg_b, flags_b, rest, Z, U, s, err);
 }
 
 // RS16_EVAL_FULL=1 (diagnostic): always the 3-kernel 65536-point eval_poly.
@@ -239,6 +240,8 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
                              rs16_error* err) {
     RS16_HIP(ws_work32.reserve(GF_ORDER * 4));
     RS16_HIP(ws_elog.reserve(GF_ORDER * 4));
+    RS16_HIP(ws_zflag.reserve(256));
+    RS16_HIP(ws_rbits.reserve(GF_ORDER / 8));
     ErasureSpec es;
     es.flags_a = flags_a;
     es.flags_b = flags_b;
@@ -247,6 +250,13 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.b_count = g.b_count;
     es.pad_fill = g.high ? 1 : 0;
     es.tail_fill = g.high ? 0 : 1;
+    // the pass metadata: received bitmap, and zero flags of the first pass's
+    // tiles (2^lo rows, lo = L/2) when the decode takes more than one pass
+    const int L = ilog2(g.n);
+    es.rbits = (uint32_t*)ws_rbits.p;
+    es.zflags = L > 8 ? (uint8_t*)ws_zflag.p : nullptr;
+    es.n = g.n;
+    es.zlo = (uint32_t)(L / 2);
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
     // 65536-row decodes run their first and last passes on 256-row tiles,
@@ -263,11 +273,11 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     return prof_end(NUM_PROGS, s, ev, err);
 }
 
-// The pass sequence of a decode, given the erasure logs in ws_elog and a
-// 256-byte zero-tile flag buffer of the caller's.
+// The pass sequence of a decode, given what decode_eval left in ws_elog /
+// ws_work32 (erasure logs), ws_rbits (received rows) and ws_zflag (zero tiles).
 int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
                                const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
-                               uint8_t* zflags, hipStream_t s, rs16_error* err) {
+                               hipStream_t s, rs16_error* err) {
     PassArgs a = base_args(this, S);
     a.seg_a = seg_a;
     a.seg_b = seg_b;
@@ -280,6 +290,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg
     a.ework = elog_fused ? (const uint32_t*)ws_work32.p : nullptr;
     a.rest = rest;
     a.rest_seg_b = g.high ? 1 : 0;
+    a.rbits = (const uint32_t*)ws_rbits.p;
     a.skew_ifft = a.skew_fft = 0;
     const int L = ilog2(g.n);
     if (L <= 8) {
@@ -289,7 +300,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg
     const int lo = L / 2, hi = L - lo;
     // One flag per DEC_FIRST tile (2^hi <= 256): tiles without a received
     // row are skipped by DEC_FIRST and read as zero by DEC_MID / DEC_LAST.
-    a.zflags = zflags;
+    a.zflags = (const uint8_t*)ws_zflag.p;
     // Launch only the tiles that can hold a received row: a segment with no
     // received shard contributes none (its tiles are flagged by block 0).
     const uint32_t tile = 1u << lo, ntiles = 1u << hi;
@@ -300,9 +311,6 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg
         t1z = std::max(t1z, std::min(ntiles, (uint32_t)(((size_t)g.chunk + g.b_count + tile - 1) / tile)));
     }
     if (t1z <= t0z) t0z = 0, t1z = 1;  // (unreachable: a decode has received shards) keep one launch
-    a.zt_lo = t0z;
-    a.zt_hi = t1z;
-    a.ztiles = ntiles;
     a.tile_base = t0z;
     a.lo = 0;
     a.out = Z;

@@ -55,9 +55,11 @@ struct rs16_engine {
     uint32_t* d_skew_entry = nullptr;
     uint32_t* d_mul_tab = nullptr;
     uint16_t* d_log_walsh = nullptr;
+    uint8_t* d_zero_sink = nullptr;  // zero page + store sink (PassArgs::zero / sink)
     // scratch
     rs16::DevBuf ws_z, ws_u, ws_fd, ws_work32, ws_elog, ws_flags;
     rs16::DevBuf ws_zflag;  // decode: per DEC_FIRST tile, 1 = no received row (tile skipped, rows zero)
+    rs16::DevBuf ws_rbits;  // decode: received-row bitmap (65536 bits)
     // Host-resident pipeline (rs16_encode_host / rs16_decode_host): column
     // slices alternate between two slots, each with its own stream and the
     // device buffers of one slice, so copies and compute of different slices
@@ -65,7 +67,7 @@ struct rs16_engine {
     // slots after the engine stream.
     struct HostSlot {
         hipStream_t s = nullptr;
-        rs16::DevBuf orig, rec, z, u, zflag;
+        rs16::DevBuf orig, rec, z, u;
     };
     HostSlot hslot[2];
     rs16::DevBuf hflags;
@@ -126,7 +128,7 @@ struct rs16_engine {
                     rs16_error* err);
     int decode_passes(const rs16::DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
                       const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
-                      uint8_t* zflags, hipStream_t s, rs16_error* err);
+                      hipStream_t s, rs16_error* err);
     // Generic (engine-op sequence) encoders, following the reference rate code.
     int encode_high_generic(size_t k, size_t m, size_t S, uint8_t* work, size_t work_count, hipStream_t s,
                             rs16_error* err);

@@ -56,6 +56,11 @@ struct PassArgs {
     uint64_t S;                // shard bytes
     uint32_t qrow;             // quads per row = S / 8
     uint32_t nslab;            // ceil(qrow / Q), set by launch_pass
+    // Persistent pass: the launch covers ntiles tiles x nslab slabs = items,
+    // item i = (tile i / nslab, slab i % nslab); workgroup b processes items
+    // [b * per_wg, (b + 1) * per_wg) in order, loading item i + 1 while it
+    // computes item i.  Set by launch_pass.
+    uint32_t ntiles, per_wg;
     uint32_t lo;               // tile bit offset
     uint32_t a_count, chunk, b_count;
     uint32_t skew_ifft, skew_fft;
@@ -66,19 +71,31 @@ struct PassArgs {
     // consumed downstream; FFT groups and stores outside it are skipped.
     // need_hi == 0: no pruning.
     uint32_t need_lo, need_hi;
-    // Decode zero tiles: zflags[t] = 1 when DEC_FIRST tile t held no received
-    // row (then it is all zero and not stored).  Written by DEC_FIRST, read by
-    // DEC_MID (row r -> flag r >> lo) and DEC_LAST; nullptr: no skipping.
-    uint8_t* zflags;
-    // DEC_FIRST is launched on tiles [zt_lo, zt_hi) only (the others cannot
-    // hold a received row: their whole segment was lost); block 0 flags the
-    // rest of the ztiles tiles as zero.
-    uint32_t zt_lo, zt_hi, ztiles;
+    // Decode zero tiles: zflags[t] = 1 when DEC_FIRST tile t holds no received
+    // row (then it is all zero after the erasure multiply and is neither
+    // computed nor stored).  Written with rbits by the eval_poly kernels from
+    // the received flags; read by DEC_FIRST (skip), DEC_MID (row r -> flag
+    // r >> lo) and DEC_LAST; nullptr: no skipping.
+    const uint8_t* zflags;
+    // Received rows of the decode as a bitmap (bit r & 31 of word r >> 5), so
+    // that a tile's flags are two scalar loads (rows of segments A and B).
+    const uint32_t* rbits;
+    // Branch-free memory access: a row that is not read (absent / zero /
+    // out-of-slab lanes) is read from `zero` (RS16_ZERO_BYTES of zeros, at
+    // offset offL & 0x7FFF), and in the pipelined build a row that is not
+    // written goes to `sink` (RS16_SINK_BYTES nobody reads), so every load
+    // and store of an item is unconditional and the compiler's vmcnt waits
+    // stay exact across the pipelined items.
+    const uint8_t* zero;
+    uint8_t* sink;
     // eval_poly with its last 256-point FWHT (row bits 0-7) left undone
     // (launch_eval_poly_from_flags, last_lo = false): DEC_FIRST / DEC_LAST at
     // T = 8 finish it for their tile's rows in LDS.  nullptr: use elog.
     const uint32_t* ework;
 };
+
+constexpr size_t RS16_ZERO_BYTES = 65536;
+constexpr size_t RS16_SINK_BYTES = 1 << 20;
 
 // Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.
 hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, hipStream_t s);
@@ -95,6 +112,12 @@ struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.r
     uint32_t a_count, chunk, b_count;
     uint32_t pad_fill;         // value of rows [a_count, chunk)   (1 for high rate)
     uint32_t tail_fill;        // value of rows >= chunk + b_count (1 for low rate)
+    // Decode pass metadata written by the same kernels (nullptr: none):
+    // rbits = received-row bitmap of rows [0, n); zflags[t] = 1 when rows
+    // [t << zlo, (t + 1) << zlo) hold no received row (t < n >> zlo <= 256).
+    uint32_t* rbits;
+    uint8_t* zflags;
+    uint32_t n, zlo;
 };
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo);

@@ -105,6 +105,39 @@ __device__ __forceinline__ uint32_t erasure_at(const ErasureSpec& e, uint32_t i)
     return e.tail_fill;
 }
 
+__device__ __forceinline__ bool received_at(const ErasureSpec& e, uint32_t i) {
+    if (i < e.a_count) return e.flags_a ? ((cu8p)e.flags_a)[i] != 0 : true;
+    if (i >= e.chunk && i - e.chunk < e.b_count) return e.flags_b ? ((cu8p)e.flags_b)[i - e.chunk] != 0 : true;
+    return false;
+}
+// Received-row bitmap and zero-tile flags of rows [base, base + 256) (a
+// 256-thread block): rbits by wave ballots, zflags per tile of 2^zlo rows.
+__device__ __forceinline__ void decode_flags_block(const ErasureSpec& e, uint32_t base) {
+    __shared__ uint32_t words[8];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const bool rcv = base + t < e.n && received_at(e, base + t);
+    const uint64_t b = __ballot(rcv);
+    if (lane == 0) {
+        words[2 * w] = (uint32_t)b;
+        words[2 * w + 1] = (uint32_t)(b >> 32);
+        if (e.rbits && base + 64 * w < e.n) {
+            e.rbits[(base >> 5) + 2 * w] = (uint32_t)b;
+            e.rbits[(base >> 5) + 2 * w + 1] = (uint32_t)(b >> 32);
+        }
+    }
+    if (!e.zflags) return;
+    __syncthreads();
+    const uint32_t ts = 1u << e.zlo, ntile = e.n >> e.zlo;
+    if (t < 256u / ts && ((base >> e.zlo) + t) < ntile) {
+        bool any = false;
+        for (uint32_t r = t * ts; r < (t + 1) * ts; r += 32) {
+            const uint32_t m = ts >= 32 ? 0xFFFFFFFFu : ((1u << ts) - 1) << (r & 31);
+            any |= (words[r >> 5] & m) != 0;
+        }
+        e.zflags[(base >> e.zlo) + t] = any ? 0 : 1;
+    }
+}
+
 // MODE 0: in = u32 work; MODE 1: build erasures from flags; MODE 2: in = u16 data.
 // OUT 0: u32 work/out; OUT 1: u16 data.
 template <int MODE, int OUT>
@@ -143,6 +176,7 @@ __global__ void __launch_bounds__(256) fwht_lo_kernel(const uint32_t* in32, cons
 __global__ void __launch_bounds__(256) fwht_lo_flags_kernel(ErasureSpec e, uint32_t* out32) {
     __shared__ uint32_t s[256];
     const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+    if (blockIdx.x * 256u < e.n) decode_flags_block(e, blockIdx.x * 256u);
     s[threadIdx.x] = erasure_at(e, idx);
     fwht256_lds(s);
     out32[idx] = s[threadIdx.x];
@@ -204,6 +238,7 @@ template <int NB>
 __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const uint16_t* log_walsh, uint32_t* z) {
     __shared__ int sh[NB][4];
     const uint32_t j = blockIdx.x, t = threadIdx.x;
+    if (j < NB) decode_flags_block(e, j * 256u);
     int v[NB];
     const bool neg1 = __builtin_popcount(j & t) & 1;
 #pragma unroll

@@ -6,24 +6,34 @@
 //
 // Structure of one pass
 // ---------------------
-//   A transform of 2^L rows runs in ceil(L/8) HBM passes.  A pass loads a
-//   tile of 2^T rows (T <= 8) x Q quads (a quad = 4 elements = one lo dword
-//   + one hi dword, rs16_gf.hpp; Q = 32 for T > 4, else 64), applies T layers
-//   and stores it.  Tile t covers rows  b_low + (k << lo) + (b_high << (lo+T)),
-//   k in [0, 2^T): lo = 0 gives contiguous tiles, lo > 0 strided ones.
+//   A transform of 2^L rows runs in ceil(L/8) HBM passes.  A pass works on
+//   items: an item is a tile of 2^T rows (T <= 8) x Q quads (a quad = 4
+//   elements = one lo dword + one hi dword, rs16_gf.hpp), loaded, run
+//   through T layers and stored.  Tile t covers rows
+//   b_low + (k << lo) + (b_high << (lo+T)), k in [0, 2^T): lo = 0 gives
+//   contiguous tiles, lo > 0 strided ones; the slab of an item selects its Q
+//   quads of the row.
+//
+//   Software pipeline: the grid is persistent (two 4-wave workgroups per CU
+//   for T >= 6).  Workgroup b takes a contiguous run of items and issues the
+//   HBM loads of item i + 1 into a second register set before it computes
+//   item i, so the loads of the next item and the stores of the previous one
+//   run under the butterflies instead of in a load phase and a store phase
+//   of their own (all workgroups of a one-item-per-workgroup grid load, then
+//   compute, then store in step).
 //
 //   Lane = quad.  Each thread keeps 16 rows ("a row set") of its quad in
-//   VGPRs; a wave holds 64/Q row sets.  The 4 layers whose row bits are in
-//   registers are radix-16 butterfly networks with no data movement; LDS
-//   transposes switch between layout A (k bits 0-3 in registers) and layout B
-//   (k bits T-4..T-1).  The transpose runs in NQR rounds of QL quads; NQR is
-//   chosen per program (Rnd below) to bound a workgroup's LDS so that several
-//   workgroups share a CU: one workgroup's HBM loads and stores overlap
-//   another's butterflies.
+//   VGPRs; a wave holds 64/Q row sets (T = 8: Q = 16, 4 row sets; T = 7:
+//   Q = 32; T = 6: Q = 64).  The 4 layers whose row bits are in registers
+//   are radix-16 butterfly networks with no data movement; an LDS transpose
+//   switches between layout A (k bits 0-3 in registers) and layout B (k bits
+//   T-4..T-1).
 //
 //   Twiddle tables: a tile needs 2^T - 1 distinct twiddles per transform
 //   direction (one per (layer, group)).  Their 80-byte v_perm multiply tables
-//   are staged into LDS once per workgroup and read with ds_read_b128
+//   are staged into LDS when a workgroup starts a new tile key (b_high: the
+//   twiddles of a strided pass are the same for every tile of a transform,
+//   so they are staged once per workgroup) and read with ds_read_b128
 //   (5 per group, broadcast within each row set), one group ahead of use.
 //   Groups are compiled as a straight-line sequence separated by register
 //   pins, so a wave holds at most two tables.  The decoder's per-row erasure
@@ -42,6 +52,8 @@
 //   DEC_MID to read those rows as zero and to skip the IFFT groups whose rows
 //   all are, and DEC_LAST that its z term is zero (y = u + L(z) = u).  At
 //   100 % original loss this is the whole original half of the decode work.
+#include <cstdlib>
+
 #include "rs16_internal.hpp"
 
 namespace rs16 {
@@ -72,18 +84,21 @@ RS16_PROG(DEC_LAST, LD_DEC_LAST, false, false, true, ST_RESTORE)
 RS16_PROG(DEC_SINGLE, LD_GATHER_DEC, true, true, true, ST_RESTORE)
 #undef RS16_PROG
 
-// Quads per tile row for T > 4 (32: a wave holds two 16-row sets of 32
-// quads; 16: four row sets of 16 quads, half-size workgroups).
-#ifndef RS16_QW
-#define RS16_QW 32
+// RS16_PIPE = 1: software-pipelined persistent passes (4-wave workgroups,
+// two per CU, the next item's rows prefetched into a second register set);
+// 0: one item per workgroup, no prefetch, 4 waves per SIMD (32 quads per
+// tile row from T = 5 on).
+#ifndef RS16_PIPE
+#define RS16_PIPE 0
 #endif
 template <int T> struct Geo {
     static constexpr int R = T > 4 ? 4 : T;               // row bits held in registers
     static constexpr int NR = 1 << R;                     // rows per thread (a row set)
-    // quads per tile row (a workgroup needs SETS >= HWS: RS16_QW < 32 from T = 6)
-    static constexpr int Q = T > 5 ? RS16_QW : (T > 4 ? 32 : 64);
-    static constexpr int HWS = 64 / Q;                    // row sets per wave
     static constexpr int SETS = 1 << (T - R);             // row sets per tile
+    // quads per tile row: PIPE: 4 waves per workgroup from T = 6 on
+    // (Q = 256 / SETS); else 32 (two 16-row sets per wave) from T = 5 on
+    static constexpr int Q = (RS16_PIPE && T >= 6) ? 256 / SETS : (T > 4 ? 32 : 64);
+    static constexpr int HWS = 64 / Q;                    // row sets per wave
     static constexpr int W = SETS / HWS > 0 ? SETS / HWS : 1;  // waves per workgroup
     static constexpr int SHB = T - R;                     // layout B: k = s + (m << SHB)
     static constexpr int THREADS = 64 * W;
@@ -92,42 +107,32 @@ template <int T> struct Geo {
     static constexpr int TSPLIT = T > 4 ? (1 << T) - (1 << (T - 4)) : 0;
 };
 
-// LDS rounds of the layout switches at T = 8 / T = 7 (diagnostic builds may
-// override them).  The programs that stage reveal tables (DEC_LAST,
-// DEC_SINGLE) keep 2 rounds at T = 8.
-#ifndef RS16_NQR8
-#define RS16_NQR8 2
-#endif
-#ifndef RS16_NQR7
-#define RS16_NQR7 2
-#endif
+// The layout switch goes through the LDS image in one round (32 KiB at
+// T = 6..8: 2^T rows x Q quads x 8 bytes).
 template <int P, int T> struct Rnd {
-    static constexpr int NQR = T == 8 ? (ProgTraits<P>::STORE == ST_RESTORE ? 2 : RS16_NQR8)
-                                      : (T == 7 ? RS16_NQR7 : 1);
+    static constexpr int NQR = (!RS16_PIPE && T >= 7) ? 2 : 1;
     static constexpr int QL = Geo<T>::Q / NQR;
 };
 
 // Dynamic LDS layout of program P at tile bits T (bytes):
-//   [region 0: data image 2^T x QL x 8 | gather multipliers 2^T x 80]
-//   [tab1: NTAB x 80][tab2: (NTAB - TSPLIT) x 80]
+//   [image: 2^T x QL x 8][ert: 2^T x 80 (gather multipliers)]
+//   [tab1: NTAB x 80 (first direction)][tab2: NTAB x 80 (second direction)]
 //   [rvt: 2^T x 80 (reveal multipliers)][lost: 2^T x u32 (row is a lost original)]
-// The gather multipliers are consumed right after the load, before the first
-// layout switch writes the image (a barrier separates the two).  tab1 holds
-// the first direction's tables; in two-direction programs tab2 holds the
-// second direction's layout-B tables and its layout-A tables are restaged
-// into tab1 once the first direction's layout-A phase is done.
+//   [elog: 256 x u32]
+// Everything but the image is per tile key and stays resident across the
+// items of that key.  At T = 8 the largest program (DEC_LAST) needs 75 KiB,
+// so two workgroups share a CU.
 template <int P, int T> struct Smem {
     using PT = ProgTraits<P>;
     static constexpr bool TWO = PT::IFFT && PT::FFT;
     static constexpr int IMG_BYTES = T > 4 ? (1 << T) * Rnd<P, T>::QL * 8 : 0;
     static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
-    static constexpr int R0_BYTES = IMG_BYTES > ERT_BYTES ? IMG_BYTES : ERT_BYTES;
+    static constexpr int ERT_OFF = IMG_BYTES;
     static constexpr int TAB1_BYTES = Geo<T>::NTAB * 80;
-    static constexpr int TAB2_BYTES = TWO ? (Geo<T>::NTAB - Geo<T>::TSPLIT) * 80 : 0;
+    static constexpr int TAB2_BYTES = TWO ? Geo<T>::NTAB * 80 : 0;
     static constexpr int RVT_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 80 : 0;
     static constexpr int LOST_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 4 : 0;
-    static constexpr int ERT_OFF = 0;
-    static constexpr int TAB1_OFF = R0_BYTES;
+    static constexpr int TAB1_OFF = ERT_OFF + ERT_BYTES;
     static constexpr int TAB2_OFF = TAB1_OFF + TAB1_BYTES;
     static constexpr int RVT_OFF = TAB2_OFF + TAB2_BYTES;
     static constexpr int LOST_OFF = RVT_OFF + RVT_BYTES;
@@ -167,27 +172,56 @@ template <int T> __device__ __forceinline__ uint32_t row_rel(const Thr& c, const
 #define RS16_NO_PIN 0
 #endif
 
-__device__ __forceinline__ void ld_quad(const uint8_t* row, const Thr& c, uint32_t& L, uint32_t& H) {
+// s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
+// (expcnt and lgkmcnt at their maxima, i.e. not waited for).
+__host__ __device__ constexpr int vmcnt_wait(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+
+// Quad loads / stores.  In the pipelined build they have no control flow: a
+// row that is not read (ok = false, or a lane past the row end) comes from
+// the zero page, a row that is not written goes to the sink (PassArgs::zero /
+// sink); the one-item build branches around them.
+__device__ __forceinline__ void ld_quad(const PassArgs& a, const uint8_t* row, bool ok, const Thr& c, uint32_t& L,
+                                        uint32_t& H) {
 #if RS16_ABLATE == 2
-    L = (uint32_t)(uintptr_t)row ^ c.offL;
+    L = (uint32_t)(uintptr_t)row ^ c.offL ^ (ok ? 1u : 0u);
     H = L * 3u;
     return;
 #endif
-    if (c.active) {
-        L = *(const uint32_t*)(row + c.offL);
-        H = *(const uint32_t*)(row + c.offL + 32);
-    } else {
-        L = H = 0;
+#if RS16_PIPE
+    const uint32_t* p = (ok && c.active) ? (const uint32_t*)(row + c.offL)
+                                         : (const uint32_t*)(a.zero + (c.offL & 0x7FFFu));
+    L = p[0];
+    H = p[8];
+#else
+    L = H = 0;
+    if (ok && c.active) {
+        const uint32_t* p = (const uint32_t*)(row + c.offL);
+        L = p[0];
+        H = p[8];
     }
+#endif
 }
-__device__ __forceinline__ void st_quad(uint8_t* row, const Thr& c, uint32_t L, uint32_t H) {
+// A dropped store: in the pipelined build it goes to the sink (2 KiB per
+// workgroup slot, so that workgroups do not all write the same lines); the
+// one-item build, which needs no exact vmcnt across items, branches.
+__device__ __forceinline__ void st_quad(const PassArgs& a, uint8_t* row, bool ok, const Thr& c, uint32_t L,
+                                        uint32_t H) {
 #if RS16_ABLATE == 2
     if ((L ^ H) != 0x9e3779b9u) return;  // keeps the results live, (almost) never stores
 #endif
-    if (c.active) {
-        *(uint32_t*)(row + c.offL) = L;
-        *(uint32_t*)(row + c.offL + 32) = H;
+#if RS16_PIPE
+    uint32_t* p = (ok && c.active)
+                      ? (uint32_t*)(row + c.offL)
+                      : (uint32_t*)(a.sink + ((blockIdx.x & (RS16_SINK_BYTES / 2048 - 1)) << 11) + (c.offL & 2047u));
+    p[0] = L;
+    p[8] = H;
+#else
+    if (ok && c.active) {
+        uint32_t* p = (uint32_t*)(row + c.offL);
+        p[0] = L;
+        p[8] = H;
     }
+#endif
 }
 
 __device__ __forceinline__ void load_table_lds(uint32_t (&t)[20], const uint4* p) {
@@ -243,8 +277,9 @@ template <int T> struct TwiddleEntry {
     uint32_t skew;
     __device__ __forceinline__ uint32_t operator()(int i) const {
         const int t = t_begin + i;
-        int kb = 0;
-        while (t >= (1 << T) - (1 << (T - kb - 1))) kb++;
+        // kb = T - 1 - floor(log2(2^T - 1 - t)) (closed form, so the staging
+        // loads of a thread issue back to back)
+        const int kb = T - 32 + __clz((uint32_t)((1 << T) - 1 - t));
         const uint32_t j = (uint32_t)(t - ((1 << T) - (1 << (T - kb))));
         const uint32_t d = 1u << (a.lo + kb);
         const uint32_t g = (c.b_high << (a.lo + T)) + (j << (kb + 1 + a.lo));
@@ -336,8 +371,8 @@ template <int T, bool LB, int KB0, int KB1, bool FFT> struct LayerSeq {
 
 // Where group G's table lives: tile group id t = offset(kb) + j, with
 // j = k >> (kb+1) of the group's rows (per row set in layout A, uniform in
-// layout B); in two-direction kernels the second direction's layout-B
-// tables are in tab2.
+// layout B); in two-direction kernels the second direction's tables are in
+// tab2.
 template <int T, bool LB, int KB0, int KB1, bool FFT, int G, bool IN_TAB2>
 __device__ __forceinline__ const uint4* group_table(const Thr& c, const uint4* tab1, const uint4* tab2) {
     using S = LayerSeq<T, LB, KB0, KB1, FFT>;
@@ -347,8 +382,7 @@ __device__ __forceinline__ const uint4* group_table(const Thr& c, const uint4* t
     // layout A: k = (s << R) + m  ->  j = (s << (R-1-kb)) + gi ; layout B: j = gi
     const uint32_t j = LB ? (uint32_t)gi : (c.s << (Geo<T>::R - 1 - kb)) + gi;
     const uint32_t t = off + j;
-    if (IN_TAB2) return tab2 + (t - Geo<T>::TSPLIT) * 5;
-    return tab1 + t * 5;
+    return (IN_TAB2 ? tab2 : tab1) + t * 5;
 }
 
 // Empty volatile asm that "redefines" the data registers: ALU work cannot
@@ -519,11 +553,13 @@ __device__ __forceinline__ void fd_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
     }
 }
 
-// Layout switch through LDS, in rounds.  `mid` runs after the first barrier
-// (every wave is past its previous phase, so that phase's tables are dead).
-template <int T, int NQR, bool FROM_B, class MID>
+// Layout switch through LDS, in rounds.  `mid` runs after the first barrier.
+struct NoMid {
+    __device__ __forceinline__ void operator()() const {}
+};
+template <int T, int NQR, bool FROM_B, class MID = NoMid>
 __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
-                                         uint2* lds, MID mid) {
+                                         uint2* lds, MID mid = MID()) {
     constexpr int QL = Geo<T>::Q / NQR;
     if (RS16_ABLATE == 4) return mid();
 #pragma unroll
@@ -535,6 +571,14 @@ __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H
         __syncthreads();
     }
 }
+
+// Two-direction programs of the one-item-per-workgroup build stage the
+// second direction's tables during the first direction (issued before the
+// first layout switch, written to LDS between its barriers), so that their
+// staging registers are not live together with the first direction's.
+template <int P, int T> struct LateS2 {
+    static constexpr bool value = ProgTraits<P>::IFFT && ProgTraits<P>::FFT && T > 4 && !RS16_PIPE;
+};
 
 // y = x + (in-tile formal derivative part) of the rows in registers, where
 // the LDS image is filled from (SL, SH) -- the rows themselves for the
@@ -559,144 +603,123 @@ __device__ __forceinline__ void tile_fd(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
     }
 }
 
-template <int P, int T>
-__global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pass_kernel(PassArgs a) {
-    using PT = ProgTraits<P>;
-    using SM = Smem<P, T>;
-    using G = Geo<T>;
-    constexpr int NR = G::NR;
-    constexpr int R = G::R;
-    constexpr int NQR = Rnd<P, T>::NQR;
-    constexpr int QL = Rnd<P, T>::QL;
-    constexpr bool TWO = SM::TWO;
-    constexpr bool ZERO_SKIP = P == DEC_MID && T > 4;  // DEC_MID runs with T >= 5 only
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint2* lds = (uint2*)smem;
-    uint4* tab1 = (uint4*)(smem + SM::TAB1_OFF);
-    uint4* tab2 = (uint4*)(smem + SM::TAB2_OFF);
-    uint4* ert = (uint4*)(smem + SM::ERT_OFF);
-    uint4* rvt = (uint4*)(smem + SM::RVT_OFF);
-    uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
+// One item's rows in registers plus what the item's load learned.
+template <int P, int T> struct ItemRegs {
+    static constexpr int NR = Geo<T>::NR;
+    static constexpr int NZ = ProgTraits<P>::LOAD == LD_DEC_LAST ? NR : 1;
+    uint32_t L[NR], H[NR];
+    uint32_t zl[NZ], zh[NZ];  // DEC_LAST: z rows for y = u + L(z)
+    uint32_t zrow, zmask;     // DEC_MID zero rows (see below)
+    bool ztile;               // DEC_LAST: z of this tile is zero (DEC_FIRST skipped it)
+};
 
-    // Block -> (tile, slab), XCD-aware: blocks are dealt to the 8 XCDs
-    // round-robin (XCD = b mod 8).  With a tile count that is a multiple of 8,
-    // all slabs of a tile run on one XCD (they share their twiddle tables in
-    // its L2) and consecutive tiles go to different XCDs, so tiles of uneven
-    // work (DEC_FIRST zero tiles, pruned rows) spread evenly over the chip.
-    const uint32_t b = blockIdx.x, ntiles = gridDim.x / a.nslab;
-    uint32_t slab, tile;
-    if ((ntiles & 7) == 0) {
-        const uint32_t i = b >> 3;
-        slab = i % a.nslab;
-        tile = (i / a.nslab) * 8 + (b & 7);
-    } else {
-        slab = b % a.nslab;
-        tile = b / a.nslab;
-    }
+// Per-item coordinates of this thread: item -> (tile, slab).
+__device__ __forceinline__ void set_item(Thr& c, const PassArgs& a, uint32_t item, uint32_t Q, uint32_t& tile,
+                                         uint32_t& slab) {
+    tile = item / a.nslab;
+    slab = item - tile * a.nslab;
     tile += a.tile_base;
-
-    Thr c;
-    c.lane = threadIdx.x & 63;
-    c.w = uni(threadIdx.x >> 6);
-    c.qt = c.lane % G::Q;
-    c.s = c.w * G::HWS + c.lane / G::Q;
-    c.ql = c.qt % QL;
-    c.round = c.qt / QL;
     c.b_low = tile & ((1u << a.lo) - 1);
     c.b_high = tile >> a.lo;
-    const uint32_t Qg = slab * G::Q + c.qt;
+    const uint32_t Qg = slab * Q + c.qt;
     c.active = Qg < a.qrow;
     c.offL = (Qg >> 3) * 64 + (Qg & 7) * 4;
+}
 
-    uint32_t L[NR], H[NR];
-    // IFFT starts with the low k bits (layout A), FFT with the high ones (B).
+// Issue the HBM loads of one item (and read its decode flags).
+template <int P, int T>
+__device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint32_t tile, ItemRegs<P, T>& d) {
+    using PT = ProgTraits<P>;
+    using G = Geo<T>;
+    constexpr int NR = G::NR, R = G::R;
     constexpr bool START_B = !PT::IFFT;
-    // Final layout: after FFT -> A; after IFFT only -> B (T > 4); T <= 4: A == B.
-    constexpr bool END_B = !PT::FFT && T > 4;
-
+    d.zrow = d.zmask = 0;
+    d.ztile = false;
     // ---------------- zero rows of DEC_MID ----------------
     // Row r of this pass came from DEC_FIRST tile r >> lo = k + (b_high << T).
     // zrow bit m: this thread's (layout-A) row m is such a skipped, zero row;
     // zmask bit j: tile rows [16j, 16j+16) all are (uniform, scalar loads).
-    uint32_t zrow = 0, zmask = 0;
-    if constexpr (ZERO_SKIP) {
+    if constexpr (P == DEC_MID && T > 4) {
         if (a.zflags) {
             const uint8_t* zt = a.zflags + (c.b_high << T);
-            const uint4 f = *(const uint4*)(zt + (c.s << R));
-            const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+            // the wave's HWS row sets are 16 * HWS consecutive flag bytes:
+            // scalar loads, then each lane picks its row set's 16
+            const cu32p zw = (cu32p)(zt + ((c.w * G::HWS) << R));
+            const uint32_t sub = c.s - c.w * G::HWS;
+            uint32_t fw[4];
 #pragma unroll
-            for (int m = 0; m < NR; m++) zrow |= ((fw[m >> 2] >> (8 * (m & 3))) & 1u) << m;
+            for (int j = 0; j < 4; j++) {
+                uint32_t v = uni(zw[j]);
+#pragma unroll
+                for (int x = 1; x < G::HWS; x++) v = sub == (uint32_t)x ? uni(zw[4 * x + j]) : v;
+                fw[j] = v;
+            }
+#pragma unroll
+            for (int m = 0; m < NR; m++) d.zrow |= ((fw[m >> 2] >> (8 * (m & 3))) & 1u) << m;
             const cu32p zf = (cu32p)zt;
 #pragma unroll
             for (int j = 0; j < G::SETS; j++)
-                if ((zf[4 * j] & zf[4 * j + 1] & zf[4 * j + 2] & zf[4 * j + 3]) == 0x01010101u) zmask |= 1u << j;
+                if ((zf[4 * j] & zf[4 * j + 1] & zf[4 * j + 2] & zf[4 * j + 3]) == 0x01010101u) d.zmask |= 1u << j;
         }
     }
-
-    // ---------------- load ----------------
-    constexpr int NZ = PT::LOAD == LD_DEC_LAST ? NR : 1;
-    uint32_t zl[NZ], zh[NZ];
-    bool rcv = false;    // DEC_FIRST: one of this thread's rows was received
-    bool ztile = false;  // DEC_LAST: z of this tile is zero (DEC_FIRST skipped the tile)
     if constexpr (PT::LOAD == LD_PLAIN) {
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            if ((zrow >> m) & 1u) L[m] = H[m] = 0;
-            else ld_quad(a.in + (uint64_t)r * a.S, c, L[m], H[m]);
+            ld_quad(a, a.in + (uint64_t)r * a.S, !((d.zrow >> m) & 1u), c, d.L[m], d.H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_ENC) {
         // HighRateEncoder::encode: work[0..k) = originals, rest zero (rate_high.rs:50-54)
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            if (r < a.a_count) ld_quad(a.seg_a + (uint64_t)r * a.S, c, L[m], H[m]);
-            else L[m] = H[m] = 0;
+            ld_quad(a, a.seg_a + (uint64_t)r * a.S, r < a.a_count, c, d.L[m], d.H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_DEC) {
-        // received rows (multiplied after the staging barrier), else zero
+        // received rows (multiplied by their erasure logs in process_item), else
+        // zero.  Received bits of the wave's rows: rows [row0, row0 + 16 HWS)
+        // of the bitmap (row0 a multiple of 16, of 32 when HWS > 1), scalar loads.
+        static_assert(START_B == false && T <= 8, "gather runs in layout A");
+        const uint32_t row0 = row_rel<T>(c, a, (c.w * G::HWS) << R);
+        const cu32p rb = (cu32p)a.rbits + (row0 >> 5);
+        const uint32_t sub = c.s - c.w * G::HWS;
+        uint32_t bits;
+        // (uni(): each word stays a scalar load; a select of two loads would
+        // be folded into one per-lane vector load)
+        if constexpr (G::HWS == 4) bits = ((sub >> 1) ? uni(rb[1]) : uni(rb[0])) >> ((sub & 1) * 16);
+        else if constexpr (G::HWS == 2) bits = uni(rb[0]) >> (sub * 16);
+        else bits = uni(rb[0]) >> (row0 & 31);
+        bits &= (1u << NR) - 1;
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            L[m] = H[m] = 0;
-            if (r < a.a_count) {
-                if (!a.flags_a || a.flags_a[r]) {
-                    rcv = true;
-                    ld_quad(a.seg_a + (uint64_t)r * a.S, c, L[m], H[m]);
-                }
-            } else if (r >= a.chunk && r - a.chunk < a.b_count) {
-                const uint32_t i = r - a.chunk;
-                if (!a.flags_b || a.flags_b[i]) {
-                    rcv = true;
-                    ld_quad(a.seg_b + (uint64_t)i * a.S, c, L[m], H[m]);
-                }
-            }
+            const bool in_b = r >= a.chunk;
+            const uint8_t* src = in_b ? a.seg_b + (uint64_t)(r - a.chunk) * a.S : a.seg_a + (uint64_t)r * a.S;
+            ld_quad(a, src, (bits >> m) & 1u, c, d.L[m], d.H[m]);
         }
     } else {  // LD_DEC_LAST: u in registers, z for y = u + L(z)
-        ztile = a.zflags && a.zflags[tile];
+        d.ztile = a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u);
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            if (ztile) zl[m] = zh[m] = 0;
-            else ld_quad(a.in + (uint64_t)r * a.S, c, zl[m], zh[m]);
-            ld_quad(a.in2 + (uint64_t)r * a.S, c, L[m], H[m]);
+            ld_quad(a, a.in + (uint64_t)r * a.S, !d.ztile, c, d.zl[m], d.zh[m]);
+            ld_quad(a, a.in2 + (uint64_t)r * a.S, true, c, d.L[m], d.H[m]);
         }
     }
-    if constexpr (P == DEC_FIRST) {
-        if (blockIdx.x == 0 && a.zflags)  // tiles not launched: their segment was lost whole
-            for (uint32_t t = threadIdx.x; t < a.ztiles; t += G::THREADS)
-                if (t < a.zt_lo || t >= a.zt_hi) a.zflags[t] = 1;
-        // A tile without received rows is zero after the erasure multiply
-        // and through the IFFT: flag it for DEC_MID / DEC_LAST and stop
-        // before staging anything.
-        const int any = __syncthreads_or(rcv ? 1 : 0);
-        if (a.zflags) {
-            if (slab == 0 && threadIdx.x == 0) a.zflags[tile] = any ? 0 : 1;
-            if (!any) return;
-        }
-    }
-    // Erasure logs of this tile's rows: the last 256-point FWHT of eval_poly,
-    // done here when the caller left it undone (ework); overlaps the tile loads.
+}
+
+// Stage everything that depends on the tile key of the thread's current
+// item: twiddle tables of both directions, and for the decoder's first /
+// last pass the per-row erasure and reveal multipliers (and the last 256-point
+// FWHT of eval_poly when the caller left it undone, ework).  Ends with a
+// barrier; the caller must have one between the previous key's last use of
+// these LDS regions and this call.
+template <int P, int T>
+__device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint32_t tile, uint8_t* smem) {
+    using PT = ProgTraits<P>;
+    using SM = Smem<P, T>;
+    using G = Geo<T>;
+    constexpr bool TWO = SM::TWO;
     const uint32_t* el = nullptr;
     if constexpr (SM::ELOG_BYTES > 0) {
         if (a.ework) {
@@ -706,32 +729,62 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
             el = elds;
         }
     }
-    // Stage the first direction's tables (and, in two-direction programs,
-    // the second direction's layout-B tables, and the decoder's per-row
-    // multipliers); their loads overlap the tile's.
-    {
-        Stager<T, G::NTAB> s1;
-        s1.issue(a, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
-        if constexpr (TWO) {
-            Stager<T, G::NTAB - G::TSPLIT> s2;
-            s2.issue(a, TwiddleEntry<T>{a, c, G::TSPLIT, a.skew_fft});
-            s2.commit(tab2);
-        }
-        if constexpr (PT::LOAD == LD_GATHER_DEC) {
-            Stager<T, (1 << T)> se;
-            se.issue(a, GatherEntry<T>{a, c, el});
-            se.commit(ert);
-        }
-        if constexpr (PT::STORE == ST_RESTORE && !(PT::FFT && T > 4)) {
-            Stager<T, (1 << T)> sr;
-            sr.issue(a, RevealEntry<T>{a, c, el});
-            const bool lf = threadIdx.x < (1u << T) && row_lost_original(a, row_rel<T>(c, a, threadIdx.x));
-            sr.commit(rvt);
-            if (threadIdx.x < (1u << T)) lostf[threadIdx.x] = lf;
-        }
-        s1.commit(tab1);
+    Stager<T, G::NTAB> s1;
+    s1.issue(a, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
+    constexpr bool S2 = TWO && !LateS2<P, T>::value;
+    Stager<T, (S2 ? G::NTAB : 0)> s2;
+    if constexpr (S2) s2.issue(a, TwiddleEntry<T>{a, c, 0, a.skew_fft});
+    if constexpr (PT::LOAD == LD_GATHER_DEC) {
+        Stager<T, (1 << T)> se;
+        se.issue(a, GatherEntry<T>{a, c, el});
+        se.commit((uint4*)(smem + SM::ERT_OFF));
     }
+    if constexpr (PT::STORE == ST_RESTORE) {
+        Stager<T, (1 << T)> sr;
+        sr.issue(a, RevealEntry<T>{a, c, el});
+        uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
+        for (uint32_t k = threadIdx.x; k < (1u << T); k += G::THREADS)
+            lostf[k] = row_lost_original(a, row_rel<T>(c, a, k));
+        sr.commit((uint4*)(smem + SM::RVT_OFF));
+    }
+    if constexpr (S2) s2.commit((uint4*)(smem + SM::TAB2_OFF));
+    s1.commit((uint4*)(smem + SM::TAB1_OFF));
     __syncthreads();  // staged tables visible
+}
+
+// Compute and store one item whose rows are in d (every thread of the
+// workgroup calls it for the same item).
+template <int P, int T>
+__device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, uint32_t tile, uint32_t slab,
+                                             ItemRegs<P, T>& d, uint8_t* smem) {
+    using PT = ProgTraits<P>;
+    using SM = Smem<P, T>;
+    using G = Geo<T>;
+    constexpr int NR = G::NR;
+    constexpr int R = G::R;
+    constexpr int NQR = Rnd<P, T>::NQR;
+    constexpr bool TWO = SM::TWO;
+    constexpr bool ZERO_SKIP = P == DEC_MID && T > 4;  // DEC_MID runs with T >= 5 only
+    uint2* lds = (uint2*)smem;
+    const uint4* tab1 = (const uint4*)(smem + SM::TAB1_OFF);
+    const uint4* tab2 = (const uint4*)(smem + SM::TAB2_OFF);
+    const uint4* ert = (const uint4*)(smem + SM::ERT_OFF);
+    const uint4* rvt = (const uint4*)(smem + SM::RVT_OFF);
+    const uint32_t* lostf = (const uint32_t*)(smem + SM::LOST_OFF);
+    uint32_t(&L)[NR] = d.L;
+    uint32_t(&H)[NR] = d.H;
+    constexpr bool START_B = !PT::IFFT;
+    // Final layout: after FFT -> A; after IFFT only -> B (T > 4); T <= 4: A == B.
+    constexpr bool END_B = !PT::FFT && T > 4;
+
+    if constexpr (P == DEC_FIRST) {
+        // A tile without received rows is zero after the erasure multiply
+        // and through the IFFT: DEC_MID / DEC_LAST read it as zero, skip it.
+        if (a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u)) {
+            __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));  // (see the end of this function)
+            return;
+        }
+    }
     if constexpr (PT::LOAD == LD_GATHER_DEC) {
 #pragma unroll
         for (int m = 0; m < NR; m++) {
@@ -743,7 +796,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
         }
     }
     if constexpr (PT::LOAD == LD_DEC_LAST) {
-        if (!ztile) tile_fd<T, NQR, START_B>(L, H, zl, zh, c, lds);
+        if (!d.ztile) tile_fd<T, NQR, START_B>(L, H, d.zl, d.zh, c, lds);
     }
 
     // ---------------- IFFT ----------------
@@ -751,21 +804,16 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
     if constexpr (PT::IFFT) {
         // DEC_MID: a wave whose rows all are zero skips its layout-A layers
         bool skip_a = false;
-        if constexpr (ZERO_SKIP) skip_a = __all(zrow == (1u << NR) - 1);
+        if constexpr (ZERO_SKIP) skip_a = __all(d.zrow == (1u << NR) - 1);
         if (!skip_a) layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
         if constexpr (T > 4) {
-            // Two-direction programs: the second direction's layout-A tables
-            // replace the first's, which are dead once every wave has passed
-            // the exchange's first barrier.
-            Stager<T, (TWO ? G::TSPLIT : 0)> s3;
-            if constexpr (TWO) s3.issue(a, TwiddleEntry<T>{a, c, 0, a.skew_fft});
-            // the gather multipliers share the image's LDS: every wave must be past them
-            if constexpr (PT::LOAD == LD_GATHER_DEC) __syncthreads();
+            Stager<T, (LateS2<P, T>::value ? G::NTAB : 0)> s2;
+            if constexpr (LateS2<P, T>::value) s2.issue(a, TwiddleEntry<T>{a, c, 0, a.skew_fft});
             exchange<T, NQR, false>(L, H, c, lds, [&]() {
-                if constexpr (TWO) s3.commit(tab1);
+                if constexpr (LateS2<P, T>::value) s2.commit((uint4*)(smem + SM::TAB2_OFF));
             });
             layers<T, true, 4, (T > 4 ? T : 4), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
-                                                                                                tab2, zmask);
+                                                                                                tab2, d.zmask);
             in_b = true;
         }
     }
@@ -777,50 +825,102 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : 4)) pa
     // ---------------- FFT ----------------
     if constexpr (PT::FFT) {
         if constexpr (T > 4) {
-            // Reveal multipliers are staged late (T > 4), to keep their
-            // registers out of the load phase.
-            Stager<T, (PT::STORE == ST_RESTORE ? (1 << T) : 0)> sr;
-            bool lf = false;
-            if constexpr (PT::STORE == ST_RESTORE) {
-                sr.issue(a, RevealEntry<T>{a, c, el});
-                lf = threadIdx.x < (1u << T) && row_lost_original(a, row_rel<T>(c, a, threadIdx.x));
-            }
             layers<T, true, 4, (T > 4 ? T : 4), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
-            exchange<T, NQR, true>(L, H, c, lds, [&]() {
-                if constexpr (PT::STORE == ST_RESTORE) {
-                    sr.commit(rvt);
-                    if (threadIdx.x < (1u << T)) lostf[threadIdx.x] = lf;
-                }
-            });
+            exchange<T, NQR, true>(L, H, c, lds);
             in_b = false;
         }
-        // two-direction, T <= 4: the whole second direction is in tab2
         bool need = true;
         if constexpr (P == DEC_MID) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
-        if (need) layers<T, false, 0, R, true, (TWO && T <= 4)>(L, H, c, a, tab1, tab2);
+        if (need) layers<T, false, 0, R, true, TWO>(L, H, c, a, tab1, tab2);
     }
 
     // ---------------- store ----------------
+    // The next item's loads were issued before this item's butterflies and
+    // have landed by now: retire them before the stores, so that the stores
+    // stay in flight across the loop latch (with 2 NR loads + 2 NR stores
+    // outstanding there, the compiler's own wait would be vmcnt(0)).
+    __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
+    // Row addresses are recomputed here from opaque copies of the item
+    // coordinates: otherwise the compiler keeps the load-time addresses of
+    // the same rows live through all the butterflies (32 VGPRs).
+    Thr cs = c;
+    asm volatile("" : "+s"(cs.b_low), "+s"(cs.b_high));
+    asm volatile("" : "+v"(cs.offL));
 #pragma unroll
     for (int m = 0; m < NR; m++) {
         const uint32_t k = kidx<T, END_B>(c, m);
-        const uint32_t r = row_rel<T>(c, a, k);
+        const uint32_t r = row_rel<T>(cs, a, k);
         if constexpr (PT::STORE == ST_PLAIN) {
-            if (P != DEC_MID || (k >= a.need_lo && k < a.need_hi)) st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
+            st_quad(a, a.out + (uint64_t)r * a.S, P != DEC_MID || (k >= a.need_lo && k < a.need_hi), cs, L[m], H[m]);
         } else if constexpr (PT::STORE == ST_RECOVERY) {
-            if (r < a.out_rows) st_quad(a.out + (uint64_t)r * a.S, c, L[m], H[m]);
+            st_quad(a, a.out + (uint64_t)r * a.S, r < a.out_rows, cs, L[m], H[m]);
         } else {
-            if (lostf[k]) {
-                uint32_t tt[20];
-                load_table_lds(tt, rvt + k * 5);
-                uint32_t ol = 0, oh = 0;
-                mul_xor(ol, oh, L[m], H[m], tt);
-                const uint32_t i = r - (a.rest_seg_b ? a.chunk : 0);
-                st_quad(a.rest + (uint64_t)i * a.S, c, ol, oh);
-            }
+            uint32_t tt[20];
+            load_table_lds(tt, rvt + k * 5);
+            uint32_t ol = 0, oh = 0;
+            mul_xor(ol, oh, L[m], H[m], tt);
+            const uint32_t i = r - (a.rest_seg_b ? a.chunk : 0);
+            st_quad(a, a.rest + (uint64_t)i * a.S, lostf[k] != 0, cs, ol, oh);
         }
     }
+}
+
+// The persistent pass: workgroup b processes items [b * per_wg, ...) of the
+// launch, loading item i + 1 while it computes item i.
+template <int P, int T>
+#ifndef RS16_MINW
+#define RS16_MINW (RS16_PIPE ? 2 : 4)
+#endif
+__global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : RS16_MINW)) pass_kernel(PassArgs a) {
+    using G = Geo<T>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const uint32_t nitems = a.ntiles * a.nslab;
+    const uint32_t it0 = blockIdx.x * a.per_wg;
+    const uint32_t it1 = min(it0 + a.per_wg, nitems);
+    if (it0 >= it1) return;  // (uniform)
+
+    Thr c;
+    c.lane = threadIdx.x & 63;
+    c.w = uni(threadIdx.x >> 6);
+    c.qt = c.lane % G::Q;
+    c.s = c.w * G::HWS + c.lane / G::Q;
+    c.ql = c.qt % Rnd<P, T>::QL;
+    c.round = c.qt / Rnd<P, T>::QL;
+
+    uint32_t tile, slab;
+    set_item(c, a, it0, G::Q, tile, slab);
+#if !RS16_PIPE
+    // one item per workgroup (launch_pass sets per_wg = 1): straight-line code
+    // (a loop lets the compiler hoist per-row address terms out of it, which
+    // costs more VGPRs than the 128 of four waves per SIMD).  The tile's
+    // loads are issued first, so the table staging overlaps their latency.
+    ItemRegs<P, T> cur;
+    load_item<P, T>(a, c, tile, cur);
+    stage_tile<P, T>(a, c, tile, smem);
+    process_item<P, T>(a, c, tile, slab, cur, smem);
+#else
+    stage_tile<P, T>(a, c, tile, smem);
+    ItemRegs<P, T> nx;
+    load_item<P, T>(a, c, tile, nx);
+    for (uint32_t it = it0; it < it1; it++) {
+        const Thr cc = c;
+        const uint32_t ctile = tile, cslab = slab;
+        ItemRegs<P, T> cur = nx;
+        const bool more = it + 1 < it1;
+        if (more) {
+            set_item(c, a, it + 1, G::Q, tile, slab);
+            load_item<P, T>(a, c, tile, nx);  // in flight during this item's butterflies
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        process_item<P, T>(a, cc, ctile, cslab, cur, smem);
+        if (more && c.b_high != cc.b_high) {
+            __syncthreads();  // every wave is done with this key's tables
+            stage_tile<P, T>(a, c, tile, smem);
+        }
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -854,11 +954,41 @@ static const int kQuads[9] = {Geo<0>::Q, Geo<1>::Q, Geo<2>::Q, Geo<3>::Q, Geo<4>
                               Geo<5>::Q, Geo<6>::Q, Geo<7>::Q, Geo<8>::Q};
 #undef RS16_TH
 
+// Resident workgroups per CU of the persistent grid (RS16_WG_PER_CU; 0 =
+// one workgroup per item).  Default: RS16_PIPE builds 2 for the 4-wave
+// workgroups of T >= 6 (8 waves and <= 150 KiB of LDS per CU), else 0.
+static int wg_per_cu(int T) {
+    static const int v = [] {
+        const char* e = std::getenv("RS16_WG_PER_CU");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (!RS16_PIPE) return 0;
+    if (v >= 0) return v;
+    return T >= 6 ? 2 : 8;
+}
+static int device_cus() {
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
 hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles, hipStream_t s) {
     if (prog < 0 || prog >= NUM_PROGS || T < 0 || T > 8) return hipErrorInvalidValue;
     if (num_tiles == 0 || args.qrow == 0) return hipSuccess;
     PassArgs a = args;
     a.nslab = (a.qrow + kQuads[T] - 1) / kQuads[T];
+    a.ntiles = num_tiles;
+    const uint64_t items = (uint64_t)num_tiles * a.nslab;
+    const int wpc = wg_per_cu(T);
+    const uint64_t max_wg = wpc > 0 ? (uint64_t)wpc * device_cus() : items;
+    a.per_wg = (uint32_t)((items + max_wg - 1) / max_wg);
+    const uint32_t nwg = (uint32_t)((items + a.per_wg - 1) / a.per_wg);
     if (a.need_hi == 0) a.need_hi = 1u << T;  // no pruning
     const size_t lds = (size_t)kSmem[prog][T];
     if (lds > 65536) {
@@ -866,7 +996,7 @@ hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles
                                            (int)lds);
         if (e != hipSuccess) return e;
     }
-    dim3 grid(num_tiles * a.nslab), block(kThreads[T]);
+    dim3 grid(nwg), block(kThreads[T]);
     hipLaunchKernelGGL(kPass[prog][T], grid, block, lds, s, a);
     return hipGetLastError();
 }
