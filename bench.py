@@ -69,9 +69,13 @@ def pass_bytes(prog: str, k: int, m: int, S: int, orig_rcv=None, rec_rcv=None) -
     """Algorithmic HBM bytes of one launch of a pass program (rows read + rows
     written, S bytes each) for a single-chunk high-rate k:m codec.  Decode
     passes follow the received masks (default: the bench's 100 % loss,
-    recovery [0, k) given): a DEC_FIRST tile without a received row is
-    neither read nor written, and its rows are not read again by DEC_MID /
-    DEC_LAST (rs16_pass.hip, "decode zero tiles")."""
+    recovery [0, k) given).  Full decode: a DEC_FIRST tile without a received
+    row is neither read nor written, and its rows are not read again by
+    DEC_MID / DEC_LAST (rs16_pass.hip, "decode zero tiles").  Half-transform
+    decode (every original lost, rs16_engine.cpp half_decode): DEC_HALF_FIRST
+    reads the received rows and writes n/2 work rows, DEC_HALF_MID reads and
+    writes n/2 rows, DEC_HALF_LAST reads the tiles that hold originals and
+    writes the lost originals."""
     import numpy as np
 
     chunk = 1 << (m - 1).bit_length()
@@ -88,7 +92,17 @@ def pass_bytes(prog: str, k: int, m: int, S: int, orig_rcv=None, rec_rcv=None) -
     tile = 1 << lo_d
     live = rcv.reshape(-1, tile).any(axis=1)  # DEC_FIRST tiles that are computed and stored
     t0, t1 = chunk // tile, -(-(chunk + k) // tile)  # DEC_LAST tiles (hold originals)
-    if prog == "ENC_FIRST":
+    h = n_dec // 2
+    lo_h = (L_dec - 1) // 2
+    if prog == "DEC_HALF_FIRST":
+        rows = int(rcv[:h].sum()) + h
+    elif prog == "DEC_HALF_MID":
+        rows = 2 * h
+    elif prog == "DEC_HALF_LAST":
+        rows = (-(-k // (1 << lo_h)) << lo_h) + int((~orig_rcv).sum())
+    elif prog == "DEC_HALF_SINGLE":
+        rows = int(rcv[:h].sum()) + int((~orig_rcv).sum())
+    elif prog == "ENC_FIRST":
         rows = k + chunk
     elif prog == "ENC_MID":
         rows = 2 * chunk

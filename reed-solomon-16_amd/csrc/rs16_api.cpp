@@ -82,7 +82,7 @@ extern "C" int rs16_engine_set_profiling(rs16_engine* e, int enable, rs16_error*
 }
 extern "C" int rs16_engine_profile_read(rs16_engine* e, int prog, double* total_ms, uint64_t* launches,
                                         rs16_error* err) {
-    if (prog < 0 || prog > NUM_PROGS) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (prog < 0 || prog >= NUM_PROF) return set_error(err, RS16_INVALID_ARGUMENT);
     if (int rc = e->activate(err)) return rc;
     if (int rc = e->prof_collect(err)) return rc;
     if (total_ms) *total_ms = e->prof_ms[prog];
@@ -93,13 +93,16 @@ extern "C" void rs16_engine_profile_reset(rs16_engine* e) {
     rs16_error err;
     (void)e->activate(&err);
     (void)e->prof_collect(&err);
-    for (int i = 0; i <= NUM_PROGS; i++) e->prof_ms[i] = 0, e->prof_n[i] = 0;
+    for (int i = 0; i < NUM_PROF; i++) e->prof_ms[i] = 0, e->prof_n[i] = 0;
 }
-extern "C" int rs16_prog_count(void) { return NUM_PROGS + 1; }
+extern "C" int rs16_prog_count(void) { return NUM_PROF; }
 extern "C" const char* rs16_prog_name(int prog) {
-    static const char* names[] = {"GEN_FFT",   "GEN_IFFT",  "ENC_FIRST", "ENC_MID",  "ENC_LAST", "ENC_SINGLE",
-                                  "DEC_FIRST", "DEC_MID",   "DEC_LAST",  "DEC_SINGLE", "EVAL_POLY"};
-    return (prog >= 0 && prog <= NUM_PROGS) ? names[prog] : "?";
+    static const char* names[] = {"GEN_FFT",   "GEN_IFFT",   "ENC_FIRST",     "ENC_MID",
+                                  "ENC_LAST",  "ENC_SINGLE", "DEC_FIRST",     "DEC_MID",
+                                  "DEC_LAST",  "DEC_SINGLE", "DEC_HALF_LAST", "DEC_HALF_SINGLE",
+                                  "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY"};
+    static_assert(sizeof names / sizeof names[0] == NUM_PROF, "profiling names");
+    return (prog >= 0 && prog < NUM_PROF) ? names[prog] : "?";
 }
 
 extern "C" const char* rs16_version(void) { return "rs16-mi355x 0.1 gfx950 (v_perm GF(2^16) engine)"; }

@@ -124,11 +124,11 @@ int rs16_engine::prof_collect(rs16_error* err) {
     return RS16_OK;
 }
 
-int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStream_t s, rs16_error* err) {
+int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStream_t s, rs16_error* err, int prof) {
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
     RS16_HIP(launch_pass(prog, T, a, tiles, s));
-    return prof_end(prog, s, ev, err);
+    return prof_end(prof < 0 ? prog : prof, s, ev, err);
 }
 
 // Engine::fft over 2^L rows: L <= 8 in one pass; otherwise the high
@@ -259,10 +259,13 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.zlo = (uint32_t)(L / 2);
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
-    // 65536-row decodes run their first and last passes on 256-row tiles,
-    // which finish eval_poly's last 256-point FWHT themselves.
-    elog_fused = ilog2(g.n) == 16;
-    if (g.high && g.n <= 2048 && !eval_full_forced()) {
+    // The decode passes that read erasure logs finish eval_poly's last
+    // 256-point FWHT themselves, for the 256-row block of their tile's rows
+    // (one kernel less) -- except the one-pass half-transform decode, whose
+    // gather and reveal rows lie in different blocks.
+    const bool small = g.high && g.n <= 2048 && !eval_full_forced();
+    elog_fused = !small && !(half_decode(g) && ilog2(g.n) - 1 <= 8);
+    if (small) {
         // erasures are zero from row n on: only n/256 live blocks (rs16_misc.hip)
         RS16_HIP(launch_eval_poly_small(es, (uint32_t)g.n, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh,
                                         s));
@@ -270,7 +273,24 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
         RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s,
                                              !elog_fused));
     }
-    return prof_end(NUM_PROGS, s, ev, err);
+    return prof_end(PROF_EVAL_POLY, s, ev, err);
+}
+
+// Half-transform decode.  When every original is lost and the originals'
+// segment is one half of the n work rows (high rate: rows [n/2, n) with
+// n = 2 chunk; low rate: rows [0, n/2)), the input of the transform is zero
+// on that half and only that half of its output is needed.  Then the top
+// layer's butterflies and every formal-derivative term cancel on the needed
+// half (see DESIGN.md "Half-transform decode"; checked against the
+// sequential oracle by tests/test_half_decode.py):
+//     FFT(FD(IFFT(x)))[dst half] = FFT_dst(IFFT_src(x[src half]))
+// with IFFT_src / FFT_dst the n/2-row transforms over the low L-1 row bits
+// with the twiddles of their half (skew_delta = its first row).  So the
+// decode is an encode-shaped pipeline on n/2 rows: gather x e -> IFFT ->
+// FFT -> reveal, with no formal derivative.
+bool rs16_engine::half_decode(const DecodeGeom& g) {
+    const bool orig_lost = g.high ? g.b_recv == 0 : g.a_recv == 0;
+    return orig_lost && g.n >= 2 && g.n == 2 * (size_t)g.chunk;
 }
 
 // The pass sequence of a decode, given what decode_eval left in ws_elog /
@@ -293,6 +313,29 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg
     a.rbits = (const uint32_t*)ws_rbits.p;
     a.skew_ifft = a.skew_fft = 0;
     const int L = ilog2(g.n);
+    if (half_decode(g)) {
+        const uint32_t half = g.n / 2, src = g.high ? 0 : half, dst = g.high ? half : 0;
+        const uint32_t orig = g.high ? g.b_count : g.a_count;
+        a.row_base_in = a.skew_ifft = src;
+        a.row_base_out = a.skew_fft = dst;
+        const int Lh = L - 1;
+        if (Lh <= 8) {
+            a.ework = nullptr;  // (decode_eval did the whole eval_poly)
+            RS16_PASS(DEC_HALF_SINGLE, Lh, a, 1, s);
+            return RS16_OK;
+        }
+        const int lo = Lh / 2, hi = Lh - lo;
+        a.lo = 0;
+        a.out = Z;
+        RS16_PASS_AS(PROF_DEC_HALF_FIRST, DEC_FIRST, lo, a, 1u << hi, s);
+        a.lo = lo;
+        a.in = Z;
+        RS16_PASS_AS(PROF_DEC_HALF_MID, ENC_MID, hi, a, 1u << lo, s);
+        a.lo = 0;
+        a.out = nullptr;
+        RS16_PASS(DEC_HALF_LAST, lo, a, (orig + (1u << lo) - 1) >> lo, s);
+        return RS16_OK;
+    }
     if (L <= 8) {
         RS16_PASS(DEC_SINGLE, L, a, 1, s);
         return RS16_OK;

@@ -29,6 +29,11 @@ int hip_fail(rs16_error* err, hipError_t e);
     do {                                                     \
         if (int _rc = this->pass(__VA_ARGS__, err)) return _rc; \
     } while (0)
+// the same under profiling id PROF
+#define RS16_PASS_AS(PROF, ...)                                     \
+    do {                                                            \
+        if (int _rc = this->pass(__VA_ARGS__, err, PROF)) return _rc; \
+    } while (0)
 
 size_t next_pow2(size_t x);
 inline int ilog2(size_t x) { int l = 0; while (((size_t)1 << l) < x) l++; return l; }
@@ -92,9 +97,10 @@ struct rs16_engine {
     std::vector<rs16_encoder*> encoders;
     std::vector<rs16_decoder*> decoders;
 
-    // Pass launch (with optional per-program hipEvent timing on the launch
-    // stream; id NUM_PROGS = the eval_poly kernels of a decode).
-    int pass(int prog, int T, const rs16::PassArgs& a, uint32_t tiles, hipStream_t s, rs16_error* err);
+    // Pass launch (with optional hipEvent timing on the launch stream under
+    // profiling id `prof` (rs16::ProfId; -1 = the program's own id).
+    int pass(int prog, int T, const rs16::PassArgs& a, uint32_t tiles, hipStream_t s, rs16_error* err,
+             int prof = -1);
     int prof_begin(hipStream_t s, hipEvent_t* ev, rs16_error* err);
     int prof_end(int id, hipStream_t s, hipEvent_t ev, rs16_error* err);
     bool profiling = false;
@@ -105,8 +111,8 @@ struct rs16_engine {
     };
     std::vector<ProfRec> prof_pending;
     std::vector<hipEvent_t> ev_pool;
-    double prof_ms[rs16::NUM_PROGS + 1] = {};
-    uint64_t prof_n[rs16::NUM_PROGS + 1] = {};
+    double prof_ms[rs16::NUM_PROF] = {};
+    uint64_t prof_n[rs16::NUM_PROF] = {};
     int prof_collect(rs16_error* err);
 
     // Engine ops on device shard arrays (validated by the C ABI layer).
@@ -129,6 +135,9 @@ struct rs16_engine {
     int decode_passes(const rs16::DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
                       const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                       hipStream_t s, rs16_error* err);
+    // The half-transform decode applies (every original lost, originals
+    // segment = one half of the work rows).
+    static bool half_decode(const rs16::DecodeGeom& g);
     // Generic (engine-op sequence) encoders, following the reference rate code.
     int encode_high_generic(size_t k, size_t m, size_t S, uint8_t* work, size_t work_count, hipStream_t s,
                             rs16_error* err);

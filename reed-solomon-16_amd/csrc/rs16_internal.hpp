@@ -38,8 +38,15 @@ enum Prog : int {
     DEC_MID,       // load -> IFFT -> (I + in-tile formal derivative) -> FFT -> store
     DEC_LAST,      // u + L(z) -> FFT -> reveal lost originals -> store them
     DEC_SINGLE,    // gather*e -> IFFT -> formal derivative -> FFT -> reveal -> store
+    // Half-transform decode (every original lost; see rs16_engine.cpp):
+    DEC_HALF_LAST,    // load -> FFT -> reveal -> store lost originals
+    DEC_HALF_SINGLE,  // gather*e -> IFFT -> FFT -> reveal -> store (one pass)
     NUM_PROGS
 };
+// Profiling ids (rs16_engine_set_profiling): the programs, then the passes
+// of the half-transform decode that reuse DEC_FIRST / ENC_MID kernels, then
+// the eval_poly kernels of a decode.
+enum ProfId : int { PROF_DEC_HALF_FIRST = NUM_PROGS, PROF_DEC_HALF_MID, PROF_EVAL_POLY, NUM_PROF };
 
 struct PassArgs {
     uint8_t* out;              // plain store base (row 0 of the transform)
@@ -66,6 +73,10 @@ struct PassArgs {
     uint32_t skew_ifft, skew_fft;
     uint32_t out_rows;         // ENC_LAST / ENC_SINGLE
     uint32_t rest_seg_b;       // originals are segment B (high rate) or A (low rate)
+    // Decode work row of pass row 0 on the gather side (received rows, their
+    // erasure logs) and on the reveal side (lost originals, their logs):
+    // 0 except in the half-transform decode.
+    uint32_t row_base_in, row_base_out;
     uint32_t tile_base;        // first tile index of this launch
     // DEC_MID output pruning: only tile rows k in [need_lo, need_hi) are
     // consumed downstream; FFT groups and stores outside it are skipped.

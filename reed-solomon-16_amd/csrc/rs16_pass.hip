@@ -82,6 +82,8 @@ RS16_PROG(DEC_FIRST, LD_GATHER_DEC, true, false, false, ST_PLAIN)
 RS16_PROG(DEC_MID, LD_PLAIN, true, true, true, ST_PLAIN)
 RS16_PROG(DEC_LAST, LD_DEC_LAST, false, false, true, ST_RESTORE)
 RS16_PROG(DEC_SINGLE, LD_GATHER_DEC, true, true, true, ST_RESTORE)
+RS16_PROG(DEC_HALF_LAST, LD_PLAIN, false, false, true, ST_RESTORE)
+RS16_PROG(DEC_HALF_SINGLE, LD_GATHER_DEC, true, false, true, ST_RESTORE)
 #undef RS16_PROG
 
 // RS16_PIPE = 1: software-pipelined persistent passes (4-wave workgroups,
@@ -137,7 +139,7 @@ template <int P, int T> struct Smem {
     static constexpr int RVT_OFF = TAB2_OFF + TAB2_BYTES;
     static constexpr int LOST_OFF = RVT_OFF + RVT_BYTES;
     // erasure logs of the tile's rows when the pass finishes eval_poly (ework)
-    static constexpr int ELOG_BYTES = ((P == DEC_FIRST || P == DEC_LAST) && T == 8) ? 256 * 4 : 0;
+    static constexpr int ELOG_BYTES = (PT::LOAD == LD_GATHER_DEC || PT::STORE == ST_RESTORE) ? 256 * 4 : 0;
     static constexpr int ELOG_OFF = LOST_OFF + LOST_BYTES;
     static constexpr int BYTES = ELOG_OFF + ELOG_BYTES;
 };
@@ -306,12 +308,14 @@ __device__ __forceinline__ bool row_lost_original(const PassArgs& a, uint32_t r)
 // row r is multiplied by erasure log e[r]; absent rows by zero.
 // e[r]: from the tile's LDS copy when the pass finished eval_poly itself
 // (el = the tile's 2^T logs), else from HBM.
+// Decoder rows: pass row r is decode work row r + row_base_in (gather side)
+// or r + row_base_out (reveal side) -- non-zero in the half-transform decode.
 template <int T> struct GatherEntry {
     const PassArgs& a;
     const Thr& c;
     const uint32_t* el;
     __device__ __forceinline__ uint32_t operator()(int k) const {
-        const uint32_t r = row_rel<T>(c, a, (uint32_t)k);
+        const uint32_t r = row_rel<T>(c, a, (uint32_t)k) + a.row_base_in;
         return row_received(a, r) ? (el ? el[k] : a.elog[r]) : ZERO_ENTRY;
     }
 };
@@ -322,20 +326,20 @@ template <int T> struct RevealEntry {
     const Thr& c;
     const uint32_t* el;
     __device__ __forceinline__ uint32_t operator()(int k) const {
-        const uint32_t r = row_rel<T>(c, a, (uint32_t)k);
+        const uint32_t r = row_rel<T>(c, a, (uint32_t)k) + a.row_base_out;
         return row_lost_original(a, r) ? GF_MODULUS - (el ? el[k] : a.elog[r]) : ZERO_ENTRY;
     }
 };
 
 // The last 256-point FWHT of eval_poly (src/engine.rs:207-218; row bits 0-7,
 // add/sub mod 65535 as NoSimd::fwht_private, src/engine/engine_nosimd.rs:153-183)
-// over a 256-row tile's values in LDS; every thread of the workgroup calls it.
-__device__ __forceinline__ void fwht256_tile(uint32_t* s) {
-    const uint32_t t = threadIdx.x;
+// over the 256-row block of a tile's rows in LDS; every thread of the
+// workgroup (NT of them) calls it.
+template <int NT> __device__ __forceinline__ void fwht256_tile(uint32_t* s) {
 #pragma unroll
     for (uint32_t d = 1; d < 256; d <<= 1) {
         __syncthreads();
-        if (t < 128) {
+        for (uint32_t t = threadIdx.x; t < 128; t += NT) {
             const uint32_t i = (t / d) * 2 * d + (t % d), j = i + d;
             const uint32_t x = s[i], y = s[j];
             s[i] = add_mod(x, y);
@@ -680,7 +684,7 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
         // zero.  Received bits of the wave's rows: rows [row0, row0 + 16 HWS)
         // of the bitmap (row0 a multiple of 16, of 32 when HWS > 1), scalar loads.
         static_assert(START_B == false && T <= 8, "gather runs in layout A");
-        const uint32_t row0 = row_rel<T>(c, a, (c.w * G::HWS) << R);
+        const uint32_t row0 = row_rel<T>(c, a, (c.w * G::HWS) << R) + a.row_base_in;
         const cu32p rb = (cu32p)a.rbits + (row0 >> 5);
         const uint32_t sub = c.s - c.w * G::HWS;
         uint32_t bits;
@@ -692,7 +696,7 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
         bits &= (1u << NR) - 1;
 #pragma unroll
         for (int m = 0; m < NR; m++) {
-            const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
+            const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m)) + a.row_base_in;
             const bool in_b = r >= a.chunk;
             const uint8_t* src = in_b ? a.seg_b + (uint64_t)(r - a.chunk) * a.S : a.seg_a + (uint64_t)r * a.S;
             ld_quad(a, src, (bits >> m) & 1u, c, d.L[m], d.H[m]);
@@ -723,10 +727,14 @@ __device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint
     const uint32_t* el = nullptr;
     if constexpr (SM::ELOG_BYTES > 0) {
         if (a.ework) {
+            // the 256-row block holding the tile's decode rows (contiguous
+            // tiles of 2^T <= 256 rows at a multiple of 2^T lie in one block)
+            const uint32_t base = PT::LOAD == LD_GATHER_DEC ? a.row_base_in : a.row_base_out;
+            const uint32_t row0 = row_rel<T>(c, a, 0) + base;
             uint32_t* elds = (uint32_t*)(smem + SM::ELOG_OFF);
-            if (threadIdx.x < 256) elds[threadIdx.x] = a.ework[(tile << 8) + threadIdx.x];
-            fwht256_tile(elds);
-            el = elds;
+            for (uint32_t i = threadIdx.x; i < 256; i += G::THREADS) elds[i] = a.ework[(row0 & ~255u) + i];
+            fwht256_tile<G::THREADS>(elds);
+            el = elds + (row0 & 255u);
         }
     }
     Stager<T, G::NTAB> s1;
@@ -744,7 +752,7 @@ __device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint
         sr.issue(a, RevealEntry<T>{a, c, el});
         uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
         for (uint32_t k = threadIdx.x; k < (1u << T); k += G::THREADS)
-            lostf[k] = row_lost_original(a, row_rel<T>(c, a, k));
+            lostf[k] = row_lost_original(a, row_rel<T>(c, a, k) + a.row_base_out);
         sr.commit((uint4*)(smem + SM::RVT_OFF));
     }
     if constexpr (S2) s2.commit((uint4*)(smem + SM::TAB2_OFF));
@@ -860,7 +868,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             load_table_lds(tt, rvt + k * 5);
             uint32_t ol = 0, oh = 0;
             mul_xor(ol, oh, L[m], H[m], tt);
-            const uint32_t i = r - (a.rest_seg_b ? a.chunk : 0);
+            const uint32_t i = r + a.row_base_out - (a.rest_seg_b ? a.chunk : 0);
             st_quad(a, a.rest + (uint64_t)i * a.S, lostf[k] != 0, cs, ol, oh);
         }
     }
@@ -872,7 +880,8 @@ template <int P, int T>
 #ifndef RS16_MINW
 #define RS16_MINW (RS16_PIPE ? 2 : 4)
 #endif
-__global__ void __launch_bounds__(Geo<T>::THREADS, (P == DEC_SINGLE ? 1 : RS16_MINW)) pass_kernel(PassArgs a) {
+__global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC_HALF_SINGLE) ? 1 : RS16_MINW))
+    pass_kernel(PassArgs a) {
     using G = Geo<T>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
@@ -934,6 +943,7 @@ typedef void (*PassFn)(PassArgs);
 static const PassFn kPass[NUM_PROGS][9] = {
     RS16_ROW(GEN_FFT),    RS16_ROW(GEN_IFFT),  RS16_ROW(ENC_FIRST), RS16_ROW(ENC_MID),  RS16_ROW(ENC_LAST),
     RS16_ROW(ENC_SINGLE), RS16_ROW(DEC_FIRST), RS16_ROW(DEC_MID),   RS16_ROW(DEC_LAST), RS16_ROW(DEC_SINGLE),
+    RS16_ROW(DEC_HALF_LAST), RS16_ROW(DEC_HALF_SINGLE),
 };
 #undef RS16_ROW
 
@@ -943,6 +953,7 @@ static const PassFn kPass[NUM_PROGS][9] = {
 static const int kSmem[NUM_PROGS][9] = {
     RS16_SM(GEN_FFT),    RS16_SM(GEN_IFFT),  RS16_SM(ENC_FIRST), RS16_SM(ENC_MID),  RS16_SM(ENC_LAST),
     RS16_SM(ENC_SINGLE), RS16_SM(DEC_FIRST), RS16_SM(DEC_MID),   RS16_SM(DEC_LAST), RS16_SM(DEC_SINGLE),
+    RS16_SM(DEC_HALF_LAST), RS16_SM(DEC_HALF_SINGLE),
 };
 #undef RS16_SM
 
