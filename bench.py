@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--original", type=int, default=32768)
     p.add_argument("--recovery", type=int, default=32768)
     p.add_argument("--shard-bytes", type=int, default=1024)
+    p.add_argument("--slices", type=int, default=1, help="concurrent column slices of the device codec")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1000:1000 side measurements")
@@ -191,6 +192,7 @@ def main():
     # RS16_BENCH_SHARE_GPU=1: every rank on GPU 0 (rehearsal of the N > 1
     # path on a one-GPU box only; the driver's N-GPU runs use one GPU per rank)
     eng = rs16.Engine(0 if os.environ.get("RS16_BENCH_SHARE_GPU") == "1" else local)
+    eng.set_slices(args.slices)
     seed = rank & 0xFF
     original = generate_original(k, S, seed)
     d_orig = DeviceArray.from_numpy(eng, original)
@@ -262,11 +264,16 @@ def main():
     dt_e = timed(encode, args.steps)
     dt_d = timed(decode, args.steps)
 
-    # ---- roofline: dominant kernel, hipEvent-timed on the engine stream ----
+    # ---- roofline: dominant kernel, hipEvent-timed on its launch stream ----
+    # (one column slice, so that every timed launch is one kernel running
+    # alone: concurrent slices would put another slice's kernels inside
+    # each event pair)
+    eng.set_slices(1)
     eng.profile_reset()
     eng.set_profiling(True)
     timed(step, args.steps)
     eng.set_profiling(False)
+    eng.set_slices(args.slices)
     prof = eng.profile()
     kernels = {name: {"avg_us": ms / n * 1e3, "launches": n} for name, (ms, n) in prof.items()}
     dom = max(prof, key=lambda p: prof[p][0])
@@ -384,7 +391,8 @@ def main():
             "data": "synthetic (ChaCha8 seed=rank stream of the reference benches; inputs resident in HBM)",
             "config": {"workload": f"{k}:{m} x {S} B encode + 100%-loss decode per GPU (BASELINE configs[3])",
                        "original_count": k, "recovery_count": m, "shard_bytes": S,
-                       "parallelism": f"independent stripes x {world} (weak, no collective)"},
+                       "parallelism": f"independent stripes x {world} (weak, no collective)",
+                       "column_slices": args.slices},
             "encode_gib_s": round(world * (k + m) * S * args.steps / dt_e / GIB, 3),
             "decode_gib_s": round(world * (k + m) * S * args.steps / dt_d / GIB, 3),
             "roofline": roofline,

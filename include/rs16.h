@@ -205,6 +205,14 @@ int rs16_decode_device(rs16_engine* eng, size_t original_count, size_t recovery_
                        void* d_original, const uint8_t* d_original_received, const void* d_recovery,
                        const uint8_t* d_recovery_received, size_t original_received_count,
                        size_t recovery_received_count, void* stream, rs16_error* err);
+/* Concurrent column slices of rs16_encode_device / rs16_decode_device (1..4,
+ * default 1): the shard columns are split into slices of multiples of 64
+ * bytes (each 64-byte column block is an independent codeword, so results
+ * are identical) that run on internal streams forked from and joined back
+ * into the call's stream.  The calls stay asynchronous and ordered on
+ * `stream`.  On MI355X / ROCm 7.2 the fork/join costs more than the overlap
+ * gains; independent codecs belong on independent streams. */
+int rs16_engine_set_slices(rs16_engine* eng, int slices, rs16_error* err);
 
 /* ---- Host-resident one-shot codec ---------------------------------------
  * reed_solomon_16::encode / decode (src/lib.rs:242-344) with every shard in
@@ -248,6 +256,12 @@ int rs16_engine_set_profiling(rs16_engine* eng, int enable, rs16_error* err);
 int rs16_engine_profile_read(rs16_engine* eng, int prog, double* total_ms, uint64_t* launches, rs16_error* err);
 void rs16_engine_profile_reset(rs16_engine* eng);
 int rs16_prog_count(void);
+/* Diagnostics: phase timeline.  Library builds made with -DRS16_STAMPS=1
+ * (scripts/stamps.py; never the shipped one) make the passes launched under
+ * profiling id `prog` write 16 u64 clock stamps per workgroup to d_buf
+ * (workgroup b at d_buf[16 b]); prog = -1 or d_buf = NULL turns it off.  Other
+ * builds accept the call and record nothing. */
+int rs16_engine_set_stamps(rs16_engine* eng, void* d_buf, int prog, rs16_error* err);
 const char* rs16_prog_name(int prog);
 
 /* Diagnostics: host-side evaluation of the device multiply (same v_perm

@@ -95,6 +95,17 @@ extern "C" void rs16_engine_profile_reset(rs16_engine* e) {
     (void)e->prof_collect(&err);
     for (int i = 0; i < NUM_PROF; i++) e->prof_ms[i] = 0, e->prof_n[i] = 0;
 }
+extern "C" int rs16_engine_set_stamps(rs16_engine* e, void* d_buf, int prog, rs16_error* err) {
+    if (prog < -1 || prog >= NUM_PROF) return set_error(err, RS16_INVALID_ARGUMENT);
+    e->stamp_buf = d_buf;
+    e->stamp_prof = prog;
+    return set_error(err, RS16_OK);
+}
+extern "C" int rs16_engine_set_slices(rs16_engine* e, int n, rs16_error* err) {
+    if (n < 1 || n > rs16_engine::MAX_SLICES) return set_error(err, RS16_INVALID_ARGUMENT);
+    e->slices = n;
+    return set_error(err, RS16_OK);
+}
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
 extern "C" const char* rs16_prog_name(int prog) {
     static const char* names[] = {"GEN_FFT",   "GEN_IFFT",   "ENC_FIRST",     "ENC_MID",
@@ -186,12 +197,12 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
     };
     if ((he = hipSetDevice(device)) != hipSuccess) return fail(he);
     if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return fail(he);
-    if ((he = hipMalloc(&e->d_skew_entry, t.skew_entry.size() * 4)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_skew_tab, (size_t)GF_ORDER * TAB_DWORDS * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_mul_tab, t.mul_tab.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_log_walsh, GF_ORDER * 2)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_zero_sink, RS16_ZERO_BYTES + RS16_SINK_BYTES)) != hipSuccess) return fail(he);
     if ((he = hipMemset(e->d_zero_sink, 0, RS16_ZERO_BYTES)) != hipSuccess) return fail(he);
-    if ((he = hipMemcpy(e->d_skew_entry, t.skew_entry.data(), t.skew_entry.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
+    if ((he = hipMemcpy(e->d_skew_tab, t.skew_tab.data(), t.skew_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_mul_tab, t.mul_tab.data(), t.mul_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_log_walsh, t.log_walsh.data(), GF_ORDER * 2, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     set_error(err, RS16_OK);
@@ -219,7 +230,12 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->hflags.release();
     if (e->hev) (void)hipEventDestroy(e->hev);
     if (e->order_ev) (void)hipEventDestroy(e->order_ev);
-    if (e->d_skew_entry) (void)hipFree(e->d_skew_entry);
+    for (int j = 0; j < rs16_engine::MAX_SLICES; j++) {
+        if (e->sl_own[j]) (void)hipStreamDestroy(e->sl_own[j]);
+        if (e->sl_join[j]) (void)hipEventDestroy(e->sl_join[j]);
+    }
+    if (e->sl_fork) (void)hipEventDestroy(e->sl_fork);
+    if (e->d_skew_tab) (void)hipFree(e->d_skew_tab);
     if (e->d_mul_tab) (void)hipFree(e->d_mul_tab);
     if (e->d_log_walsh) (void)hipFree(e->d_log_walsh);
     if (e->d_zero_sink) (void)hipFree(e->d_zero_sink);
@@ -409,7 +425,7 @@ extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
     const size_t chunk = next_pow2(enc->m);
     int rc;
     if (enc->high && enc->k <= chunk)
-        rc = e->encode_high_fused(enc->k, enc->m, enc->S, w, w, w, e->stream, err);
+        rc = e->encode_high_fused(enc->k, enc->m, enc->S, enc->S, w, w, w, e->stream, err);
     else if (enc->high)
         rc = e->encode_high_generic(enc->k, enc->m, enc->S, w, enc->work_count, e->stream, err);
     else
@@ -560,7 +576,7 @@ extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
     RS16_HIP(hipMemcpyAsync(fl, d->received.data(), g.a_count, hipMemcpyHostToDevice, e->stream));
     RS16_HIP(hipMemcpyAsync(fl + GF_ORDER, d->received.data() + g.chunk, g.b_count, hipMemcpyHostToDevice, e->stream));
     uint8_t* w = (uint8_t*)d->work.p;
-    if (int rc = e->decode_fused(g, d->S, w, fl, w + (size_t)g.chunk * d->S, fl + GF_ORDER, w + d->orig_base * d->S,
+    if (int rc = e->decode_fused(g, d->S, d->S, w, fl, w + (size_t)g.chunk * d->S, fl + GF_ORDER, w + d->orig_base * d->S,
                                  w, (uint8_t*)d->ubuf.p, e->stream, err))
         return rc;
     RS16_HIP(hipStreamSynchronize(e->stream));  // host flag buffers are pageable
@@ -597,7 +613,7 @@ extern "C" int rs16_decoder_is_high_rate(const rs16_decoder* d) { return d->high
 // work_count x S bytes, on stream s.
 static int encode_dev(rs16_engine* e, bool high, size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec,
                       uint8_t* Z, hipStream_t s, rs16_error* err) {
-    if (high && k <= next_pow2(m)) return e->encode_high_fused(k, m, S, d_orig, d_rec, Z, s, err);
+    if (high && k <= next_pow2(m)) return e->encode_high_fused(k, m, S, S, d_orig, d_rec, Z, s, err);
     const size_t wc = rs16_encoder_work_count(high, k, m);
     RS16_HIP(hipMemcpyAsync(Z, d_orig, k * S, hipMemcpyDeviceToDevice, s));
     int rc = high ? e->encode_high_generic(k, m, S, Z, wc, s, err) : e->encode_low_generic(k, m, S, Z, wc, s, err);
@@ -613,10 +629,26 @@ extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);
     if (int rc = e->order(s, err)) return rc;
-    RS16_HIP(e->ws_z.reserve(rs16_encoder_work_count(high, k, m) * S));
-    if (int rc = encode_dev(e, high, k, m, S, (const uint8_t*)d_original, (uint8_t*)d_recovery,
-                            (uint8_t*)e->ws_z.p, s, err))
-        return rc;
+    const size_t wc = rs16_encoder_work_count(high, k, m);
+    RS16_HIP(e->ws_z.reserve(wc * S));
+    const int n = (high && k <= next_pow2(m)) ? e->slice_count(S) : 1;
+    if (n == 1) {
+        if (int rc = encode_dev(e, high, k, m, S, (const uint8_t*)d_original, (uint8_t*)d_recovery,
+                                (uint8_t*)e->ws_z.p, s, err))
+            return rc;
+        return set_error(err, RS16_OK);
+    }
+    // column slices on the engine's slice streams (work space: wc x width each)
+    if (int rc = e->fork(s, n, err)) return rc;
+    const size_t blocks = S / 64;
+    for (int j = 0, b0 = 0; j < n; j++) {
+        const size_t b1 = blocks * (j + 1) / n, off = b0 * 64, w = (b1 - b0) * 64;
+        if (int rc = e->encode_high_fused(k, m, w, S, (const uint8_t*)d_original + off, (uint8_t*)d_recovery + off,
+                                          (uint8_t*)e->ws_z.p + wc * off, e->sl_stream[j], err))
+            return rc;
+        b0 = (int)b1;
+    }
+    if (int rc = e->join(s, n, err)) return rc;
     return set_error(err, RS16_OK);
 }
 
@@ -714,7 +746,7 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
                                       hipMemcpyHostToDevice, sl.s));
         const uint8_t* o = (const uint8_t*)sl.orig.p;
         const uint8_t* r = (const uint8_t*)sl.rec.p;
-        if (int rc = e->decode_passes(g, w, high ? r : o, fa, high ? o : r, fb, (uint8_t*)sl.orig.p,
+        if (int rc = e->decode_passes(g, w, w, high ? r : o, fa, high ? o : r, fb, (uint8_t*)sl.orig.p,
                                       (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, sl.s, err))
             return rc;
         // restored originals land in place; received rows come back unchanged
@@ -743,11 +775,30 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     RS16_HIP(e->ws_u.reserve((size_t)g.n * S));
     const uint8_t* orig = (const uint8_t*)d_original;
     const uint8_t* rec = (const uint8_t*)d_recovery;
-    int rc = high ? e->decode_fused(g, S, rec, d_recovery_received, orig, d_original_received, (uint8_t*)d_original,
-                                    (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p, s, err)
-                  : e->decode_fused(g, S, orig, d_original_received, rec, d_recovery_received, (uint8_t*)d_original,
-                                    (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p, s, err);
-    if (rc) return rc;
+    const uint8_t* seg_a = high ? rec : orig;
+    const uint8_t* seg_b = high ? orig : rec;
+    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
+    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
+    // erasure logs once, then the passes per column slice on the slice streams
+    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err)) return rc;
+    const int n = e->slice_count(S);
+    if (n == 1) {
+        if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
+                                      (uint8_t*)e->ws_u.p, s, err))
+            return rc;
+        return set_error(err, RS16_OK);
+    }
+    if (int rc = e->fork(s, n, err)) return rc;
+    const size_t blocks = S / 64;
+    for (int j = 0, b0 = 0; j < n; j++) {
+        const size_t b1 = blocks * (j + 1) / n, off = b0 * 64, w = (b1 - b0) * 64;
+        if (int rc = e->decode_passes(g, w, S, seg_a + off, fl_a, seg_b + off, fl_b, (uint8_t*)d_original + off,
+                                      (uint8_t*)e->ws_z.p + (size_t)g.n * off, (uint8_t*)e->ws_u.p + (size_t)g.n * off,
+                                      e->sl_stream[j], err))
+            return rc;
+        b0 = (int)b1;
+    }
+    if (int rc = e->join(s, n, err)) return rc;
     return set_error(err, RS16_OK);
 }
 

@@ -53,11 +53,11 @@ DecodeGeom decode_geom(bool high, size_t k, size_t m) {
 static PassArgs base_args(const rs16_engine* e, size_t S) {
     PassArgs a;
     std::memset(&a, 0, sizeof a);
-    a.skew_entry = e->d_skew_entry;
+    a.skew_tab = e->d_skew_tab;
     a.mul_tab = e->d_mul_tab;
     a.zero = e->d_zero_sink;
     a.sink = e->d_zero_sink + RS16_ZERO_BYTES;
-    a.S = S;
+    a.S_in = a.S_out = a.S_seg = a.S_rest = S;
     a.qrow = (uint32_t)(S / 8);
     return a;
 }
@@ -68,6 +68,38 @@ using namespace rs16;
 
 int rs16_engine::activate(rs16_error* err) {
     RS16_HIP(hipSetDevice(device));
+    return RS16_OK;
+}
+
+int rs16_engine::slice_count(size_t S) const {
+    static const int env = [] {
+        const char* v = std::getenv("RS16_SLICES");
+        return v ? std::atoi(v) : 0;
+    }();
+    const int n = env > 0 ? env : slices;
+    return (int)std::max<size_t>(1, std::min<size_t>(std::min(n, MAX_SLICES), S / 64));
+}
+
+// Slice 0 runs on the caller's stream s itself; slices 1.. on sl_stream[1..]
+// (sl_stream[0] = s while a sliced call is being issued).
+int rs16_engine::fork(hipStream_t s, int n, rs16_error* err) {
+    if (!sl_fork) RS16_HIP(hipEventCreateWithFlags(&sl_fork, hipEventDisableTiming));
+    if (n > 1) RS16_HIP(hipEventRecord(sl_fork, s));
+    for (int j = 1; j < n; j++) {
+        if (!sl_own[j]) RS16_HIP(hipStreamCreateWithFlags(&sl_own[j], hipStreamNonBlocking));
+        RS16_HIP(hipStreamWaitEvent(sl_own[j], sl_fork, 0));
+    }
+    sl_stream[0] = s;
+    for (int j = 1; j < MAX_SLICES; j++) sl_stream[j] = sl_own[j];
+    return RS16_OK;
+}
+
+int rs16_engine::join(hipStream_t s, int n, rs16_error* err) {
+    for (int j = 1; j < n; j++) {
+        if (!sl_join[j]) RS16_HIP(hipEventCreateWithFlags(&sl_join[j], hipEventDisableTiming));
+        RS16_HIP(hipEventRecord(sl_join[j], sl_own[j]));
+        RS16_HIP(hipStreamWaitEvent(s, sl_join[j], 0));
+    }
     return RS16_OK;
 }
 
@@ -126,9 +158,16 @@ int rs16_engine::prof_collect(rs16_error* err) {
 
 int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStream_t s, rs16_error* err, int prof) {
     hipEvent_t ev;
+    if (prof < 0) prof = prog;
     if (int rc = prof_begin(s, &ev, err)) return rc;
-    RS16_HIP(launch_pass(prog, T, a, tiles, s));
-    return prof_end(prof < 0 ? prog : prof, s, ev, err);
+    if (stamp_buf && prof == stamp_prof) {
+        PassArgs b = a;
+        b.stamps = (uint64_t*)stamp_buf;
+        RS16_HIP(launch_pass(prog, T, b, tiles, s));
+    } else {
+        RS16_HIP(launch_pass(prog, T, a, tiles, s));
+    }
+    return prof_end(prof, s, ev, err);
 }
 
 // Engine::fft over 2^L rows: L <= 8 in one pass; otherwise the high
@@ -175,18 +214,20 @@ int rs16_engine::ifft(uint8_t* data, size_t S, size_t pos, size_t size, size_t s
 //   recovery = FFT(IFFT(originals zero-padded to chunk, skew = chunk), skew = 0)[0..m)
 // as three passes over the 2-D row factorisation (contiguous low bits /
 // strided high bits); IFFT-high and FFT-high share the strided pass.
-int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
+int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
                                    hipStream_t s, rs16_error* err) {
     const size_t chunk = next_pow2(m);
     const int L = ilog2(chunk);
     PassArgs a = base_args(this, S);
     a.seg_a = d_orig;
+    a.S_seg = S_user;
     a.a_count = (uint32_t)k;
     a.skew_ifft = (uint32_t)chunk;
     a.skew_fft = 0;
     a.out_rows = (uint32_t)m;
     if (L <= 8) {
         a.out = d_rec;
+        a.S_out = S_user;
         RS16_PASS(ENC_SINGLE, L, a, 1, s);
         return RS16_OK;
     }
@@ -204,6 +245,7 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* 
     RS16_PASS(ENC_MID, hi, a, 1u << lo, s);
     a.in = Z;
     a.out = d_rec;
+    a.S_out = S_user;
     a.lo = 0;
     const uint32_t tiles = (uint32_t)((m + ((size_t)1 << lo) - 1) >> lo);
     RS16_PASS(ENC_LAST, lo, a, tiles, s);
@@ -219,11 +261,11 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* 
 // where the formal derivative FD = I + L + H is split into its low-bit part L
 // and high-bit part H (L commutes with the high-bit layers and
 // FFT_high o IFFT_high = I), so no separate derivative pass is needed.
-int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                               const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                               hipStream_t s, rs16_error* err) {
     if (int rc = decode_eval(g, flags_a, flags_b, s, err)) return rc;
-    return decode_passes(g, S, seg_a, flags_a, seg_b, flags_b, rest, Z, U, s, err);
+    return decode_passes(g, S, S_user, seg_a, flags_a, seg_b, flags_b, rest, Z, U, s, err);
 }
 
 // RS16_EVAL_FULL=1 (diagnostic): always the 3-kernel 65536-point eval_poly.
@@ -295,10 +337,11 @@ bool rs16_engine::half_decode(const DecodeGeom& g) {
 
 // The pass sequence of a decode, given what decode_eval left in ws_elog /
 // ws_work32 (erasure logs), ws_rbits (received rows) and ws_zflag (zero tiles).
-int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                                const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                                hipStream_t s, rs16_error* err) {
     PassArgs a = base_args(this, S);
+    a.S_seg = a.S_rest = S_user;
     a.seg_a = seg_a;
     a.seg_b = seg_b;
     a.flags_a = flags_a;

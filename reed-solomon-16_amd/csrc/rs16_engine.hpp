@@ -57,7 +57,7 @@ struct rs16_decoder;
 struct rs16_engine {
     int device = 0;
     hipStream_t stream = nullptr;
-    uint32_t* d_skew_entry = nullptr;
+    uint32_t* d_skew_tab = nullptr;  // v_perm table per twiddle index (8 MiB)
     uint32_t* d_mul_tab = nullptr;
     uint16_t* d_log_walsh = nullptr;
     uint8_t* d_zero_sink = nullptr;  // zero page + store sink (PassArgs::zero / sink)
@@ -75,6 +75,22 @@ struct rs16_engine {
         rs16::DevBuf orig, rec, z, u;
     };
     HostSlot hslot[2];
+    // Column slices of the device-resident one-shot codec: a stripe's shard
+    // columns are split into `slices` slices (multiples of 64 bytes; every
+    // 64-byte column block is an independent codeword) that run on internal
+    // streams forked from and joined back into the caller's stream.  Default
+    // 1: measured on MI355X (scripts/probe_fork.py), the fork/join events
+    // cost ~8 us of host time each and the cross-queue dependencies erase the
+    // overlap (32768:32768 x 1 KiB encode 97 us at 1 slice, 101 us at 2);
+    // only fully independent streams (two stripes) gain (+10 %).
+    static constexpr int MAX_SLICES = 4;
+    int slices = 1;
+    hipStream_t sl_stream[MAX_SLICES] = {};  // per call: [0] = caller's stream, [j] = sl_own[j]
+    hipStream_t sl_own[MAX_SLICES] = {};
+    hipEvent_t sl_fork = nullptr, sl_join[MAX_SLICES] = {};
+    int slice_count(size_t S) const;
+    int fork(hipStream_t s, int n, rs16_error* err);
+    int join(hipStream_t s, int n, rs16_error* err);
     rs16::DevBuf hflags;
     hipEvent_t hev = nullptr;
     int host_slots(rs16_error* err);
@@ -104,6 +120,10 @@ struct rs16_engine {
     int prof_begin(hipStream_t s, hipEvent_t* ev, rs16_error* err);
     int prof_end(int id, hipStream_t s, hipEvent_t ev, rs16_error* err);
     bool profiling = false;
+    // diagnostic timelines (rs16_engine_set_stamps): passes under profiling
+    // id stamp_prof get stamp_buf (RS16_STAMPS builds record into it)
+    void* stamp_buf = nullptr;
+    int stamp_prof = -1;
     bool elog_fused = false;  // last decode_eval left the final 256-point FWHT to the passes (ws_work32)
     struct ProfRec {
         int id;
@@ -121,18 +141,21 @@ struct rs16_engine {
 
     // Fused HighRate single-chunk encode: originals rows [0,k) of d_orig ->
     // recovery rows [0,m) of d_rec, using Z (chunk rows) as work.
-    int encode_high_fused(size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
+    // S = row width worked on (a column slice of the caller's arrays when
+    // S < S_user), S_user = row stride of d_orig / d_rec (Z: stride S).
+    int encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
                           hipStream_t s, rs16_error* err);
     // Fused decode (both rates): seg_a / seg_b gather sources with device
     // flags; lost originals written to rest; Z, U work (n rows each; Z may
     // alias the sources when they live at their work positions).
-    int decode_fused(const rs16::DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+    // S = row width, S_user = row stride of seg_a / seg_b / rest (Z, U: stride S)
+    int decode_fused(const rs16::DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                      const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                      hipStream_t s, rs16_error* err);
     // decode_fused = decode_eval (erasure logs into ws_elog) + decode_passes.
     int decode_eval(const rs16::DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
                     rs16_error* err);
-    int decode_passes(const rs16::DecodeGeom& g, size_t S, const uint8_t* seg_a, const uint8_t* flags_a,
+    int decode_passes(const rs16::DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                       const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                       hipStream_t s, rs16_error* err);
     // The half-transform decode applies (every original lost, originals

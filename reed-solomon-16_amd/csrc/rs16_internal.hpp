@@ -15,6 +15,7 @@ struct HostTables {
     std::vector<uint16_t> exp, log, skew, log_walsh;
     std::vector<uint32_t> skew_entry;  // GF_ORDER entries: mul-table entry of each twiddle
     std::vector<uint32_t> mul_tab;     // TAB_ENTRIES * TAB_DWORDS
+    std::vector<uint32_t> skew_tab;    // GF_ORDER * TAB_DWORDS: mul_tab row of skew_entry[i]
 };
 const HostTables& host_tables();
 
@@ -58,10 +59,13 @@ struct PassArgs {
     const uint8_t* flags_b;    // received flags of segment B
     uint8_t* rest;             // restored-originals output (row 0 = original 0)
     const uint32_t* elog;      // erasure logs by row (eval_poly output)
-    const uint32_t* skew_entry;
-    const uint32_t* mul_tab;
-    uint64_t S;                // shard bytes
-    uint32_t qrow;             // quads per row = S / 8
+    const uint32_t* skew_tab;   // v_perm table of every twiddle index: GF_ORDER x TAB_DWORDS
+    const uint32_t* mul_tab;    // v_perm table of every log (TAB_ENTRIES x TAB_DWORDS)
+    // Row strides (bytes) of in / in2, out, seg_a / seg_b and rest: equal to
+    // the row width for work arrays, the caller's shard_bytes for its arrays
+    // when the pass works on a column slice of them.
+    uint64_t S_in, S_out, S_seg, S_rest;
+    uint32_t qrow;             // quads per row of the slice = width / 8
     uint32_t nslab;            // ceil(qrow / Q), set by launch_pass
     // Persistent pass: the launch covers ntiles tiles x nslab slabs = items,
     // item i = (tile i / nslab, slab i % nslab); workgroup b processes items
@@ -103,6 +107,8 @@ struct PassArgs {
     // (launch_eval_poly_from_flags, last_lo = false): DEC_FIRST / DEC_LAST at
     // T = 8 finish it for their tile's rows in LDS.  nullptr: use elog.
     const uint32_t* ework;
+    // diagnostic timeline buffer (RS16_STAMPS builds; nullptr otherwise)
+    uint64_t* stamps;
 };
 
 constexpr size_t RS16_ZERO_BYTES = 65536;

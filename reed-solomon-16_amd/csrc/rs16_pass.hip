@@ -174,6 +174,26 @@ template <int T> __device__ __forceinline__ uint32_t row_rel(const Thr& c, const
 #define RS16_NO_PIN 0
 #endif
 
+// Diagnostic timeline build (-DRS16_STAMPS=1, never the shipped library):
+// wave 0 of every workgroup stores s_memtime at phase boundaries to
+// stamps[block * 16 + phase] (phase 15: s_memrealtime at the end, 14 at
+// the start, for the clock).  scripts/stamps.py reads them.
+#ifndef RS16_STAMPS
+#define RS16_STAMPS 0
+#endif
+__device__ __forceinline__ void stamp(const PassArgs& a, int i) {
+#if RS16_STAMPS
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
+        if (i == 0) a.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+        if (i == 11) a.stamps[blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+    }
+#else
+    (void)a;
+    (void)i;
+#endif
+}
+
 // s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
 // (expcnt and lgkmcnt at their maxima, i.e. not waited for).
 __host__ __device__ constexpr int vmcnt_wait(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
@@ -249,9 +269,10 @@ template <int T, int N> struct Stager {
     static constexpr int PER = (N * 5 + Geo<T>::THREADS - 1) / Geo<T>::THREADS;
     u32x4 v[PER > 0 ? PER : 1];
 
-    template <class F> __device__ __forceinline__ void issue(const PassArgs& a, F entry) {
+    // table i = entry(i) of `tabs` (TAB_DWORDS dwords per entry)
+    template <class F> __device__ __forceinline__ void issue(const uint32_t* tabs, F entry) {
         if (RS16_ABLATE == 3) return;
-        const u32x4* tab = (const u32x4*)a.mul_tab;
+        const u32x4* tab = (const u32x4*)tabs;
 #pragma unroll
         for (int i = 0; i < PER; i++) {
             const int idx = (int)threadIdx.x + i * Geo<T>::THREADS;
@@ -269,7 +290,8 @@ template <int T, int N> struct Stager {
     }
 };
 
-// Twiddle of tile group t (t in [0, 2^T - 1)): layer kb with
+// Twiddle of tile group t (t in [0, 2^T - 1)) as an index of skew_tab (the
+// v_perm table of every skew entry, so staging is one load deep): layer kb with
 // offset(kb) = 2^T - 2^(T-kb) <= t < offset(kb+1), group j = t - offset(kb)
 // covering tile rows k with k >> (kb+1) == j.
 template <int T> struct TwiddleEntry {
@@ -285,7 +307,7 @@ template <int T> struct TwiddleEntry {
         const uint32_t j = (uint32_t)(t - ((1 << T) - (1 << (T - kb))));
         const uint32_t d = 1u << (a.lo + kb);
         const uint32_t g = (c.b_high << (a.lo + T)) + (j << (kb + 1 + a.lo));
-        return a.skew_entry[g + d + skew - 1];
+        return g + d + skew - 1;
     }
 };
 
@@ -670,14 +692,14 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a, a.in + (uint64_t)r * a.S, !((d.zrow >> m) & 1u), c, d.L[m], d.H[m]);
+            ld_quad(a, a.in + (uint64_t)r * a.S_in, !((d.zrow >> m) & 1u), c, d.L[m], d.H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_ENC) {
         // HighRateEncoder::encode: work[0..k) = originals, rest zero (rate_high.rs:50-54)
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a, a.seg_a + (uint64_t)r * a.S, r < a.a_count, c, d.L[m], d.H[m]);
+            ld_quad(a, a.seg_a + (uint64_t)r * a.S_seg, r < a.a_count, c, d.L[m], d.H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_DEC) {
         // received rows (multiplied by their erasure logs in process_item), else
@@ -698,7 +720,7 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m)) + a.row_base_in;
             const bool in_b = r >= a.chunk;
-            const uint8_t* src = in_b ? a.seg_b + (uint64_t)(r - a.chunk) * a.S : a.seg_a + (uint64_t)r * a.S;
+            const uint8_t* src = in_b ? a.seg_b + (uint64_t)(r - a.chunk) * a.S_seg : a.seg_a + (uint64_t)r * a.S_seg;
             ld_quad(a, src, (bits >> m) & 1u, c, d.L[m], d.H[m]);
         }
     } else {  // LD_DEC_LAST: u in registers, z for y = u + L(z)
@@ -706,8 +728,8 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a, a.in + (uint64_t)r * a.S, !d.ztile, c, d.zl[m], d.zh[m]);
-            ld_quad(a, a.in2 + (uint64_t)r * a.S, true, c, d.L[m], d.H[m]);
+            ld_quad(a, a.in + (uint64_t)r * a.S_in, !d.ztile, c, d.zl[m], d.zh[m]);
+            ld_quad(a, a.in2 + (uint64_t)r * a.S_in, true, c, d.L[m], d.H[m]);
         }
     }
 }
@@ -715,49 +737,62 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
 // Stage everything that depends on the tile key of the thread's current
 // item: twiddle tables of both directions, and for the decoder's first /
 // last pass the per-row erasure and reveal multipliers (and the last 256-point
-// FWHT of eval_poly when the caller left it undone, ework).  Ends with a
-// barrier; the caller must have one between the previous key's last use of
-// these LDS regions and this call.
-template <int P, int T>
-__device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint32_t tile, uint8_t* smem) {
+// FWHT of eval_poly when the caller left it undone, ework).  In two steps:
+// issue() sends the twiddle-table loads (one level deep, from skew_tab), so
+// the caller can issue the tile's data loads behind them; finish() stages the
+// per-row multipliers, writes everything to LDS and ends with a barrier.  The
+// caller must have a barrier between the previous key's last use of these
+// LDS regions and finish().
+template <int P, int T> struct TileStage {
     using PT = ProgTraits<P>;
     using SM = Smem<P, T>;
     using G = Geo<T>;
-    constexpr bool TWO = SM::TWO;
-    const uint32_t* el = nullptr;
-    if constexpr (SM::ELOG_BYTES > 0) {
-        if (a.ework) {
-            // the 256-row block holding the tile's decode rows (contiguous
-            // tiles of 2^T <= 256 rows at a multiple of 2^T lie in one block)
-            const uint32_t base = PT::LOAD == LD_GATHER_DEC ? a.row_base_in : a.row_base_out;
-            const uint32_t row0 = row_rel<T>(c, a, 0) + base;
-            uint32_t* elds = (uint32_t*)(smem + SM::ELOG_OFF);
-            for (uint32_t i = threadIdx.x; i < 256; i += G::THREADS) elds[i] = a.ework[(row0 & ~255u) + i];
-            fwht256_tile<G::THREADS>(elds);
-            el = elds + (row0 & 255u);
-        }
-    }
+    static constexpr bool S2 = SM::TWO && !LateS2<P, T>::value;
     Stager<T, G::NTAB> s1;
-    s1.issue(a, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
-    constexpr bool S2 = TWO && !LateS2<P, T>::value;
     Stager<T, (S2 ? G::NTAB : 0)> s2;
-    if constexpr (S2) s2.issue(a, TwiddleEntry<T>{a, c, 0, a.skew_fft});
-    if constexpr (PT::LOAD == LD_GATHER_DEC) {
-        Stager<T, (1 << T)> se;
-        se.issue(a, GatherEntry<T>{a, c, el});
-        se.commit((uint4*)(smem + SM::ERT_OFF));
+
+    __device__ __forceinline__ void issue(const PassArgs& a, const Thr& c) {
+        s1.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
+        if constexpr (S2) s2.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
     }
-    if constexpr (PT::STORE == ST_RESTORE) {
-        Stager<T, (1 << T)> sr;
-        sr.issue(a, RevealEntry<T>{a, c, el});
-        uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
-        for (uint32_t k = threadIdx.x; k < (1u << T); k += G::THREADS)
-            lostf[k] = row_lost_original(a, row_rel<T>(c, a, k) + a.row_base_out);
-        sr.commit((uint4*)(smem + SM::RVT_OFF));
+    __device__ __forceinline__ void finish(const PassArgs& a, const Thr& c, uint8_t* smem) {
+        const uint32_t* el = nullptr;
+        if constexpr (SM::ELOG_BYTES > 0) {
+            if (a.ework) {
+                // the 256-row block holding the tile's decode rows (contiguous
+                // tiles of 2^T <= 256 rows at a multiple of 2^T lie in one block)
+                const uint32_t base = PT::LOAD == LD_GATHER_DEC ? a.row_base_in : a.row_base_out;
+                const uint32_t row0 = row_rel<T>(c, a, 0) + base;
+                uint32_t* elds = (uint32_t*)(smem + SM::ELOG_OFF);
+                for (uint32_t i = threadIdx.x; i < 256; i += G::THREADS) elds[i] = a.ework[(row0 & ~255u) + i];
+                fwht256_tile<G::THREADS>(elds);
+                el = elds + (row0 & 255u);
+            }
+        }
+        if constexpr (PT::LOAD == LD_GATHER_DEC) {
+            Stager<T, (1 << T)> se;
+            se.issue(a.mul_tab, GatherEntry<T>{a, c, el});
+            se.commit((uint4*)(smem + SM::ERT_OFF));
+        }
+        if constexpr (PT::STORE == ST_RESTORE) {
+            Stager<T, (1 << T)> sr;
+            sr.issue(a.mul_tab, RevealEntry<T>{a, c, el});
+            uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
+            for (uint32_t k = threadIdx.x; k < (1u << T); k += G::THREADS)
+                lostf[k] = row_lost_original(a, row_rel<T>(c, a, k) + a.row_base_out);
+            sr.commit((uint4*)(smem + SM::RVT_OFF));
+        }
+        if constexpr (S2) s2.commit((uint4*)(smem + SM::TAB2_OFF));
+        s1.commit((uint4*)(smem + SM::TAB1_OFF));
+        __syncthreads();  // staged tables visible
     }
-    if constexpr (S2) s2.commit((uint4*)(smem + SM::TAB2_OFF));
-    s1.commit((uint4*)(smem + SM::TAB1_OFF));
-    __syncthreads();  // staged tables visible
+};
+template <int P, int T>
+__device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint32_t tile, uint8_t* smem) {
+    (void)tile;
+    TileStage<P, T> st;
+    st.issue(a, c);
+    st.finish(a, c, smem);
 }
 
 // Compute and store one item whose rows are in d (every thread of the
@@ -814,33 +849,40 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         bool skip_a = false;
         if constexpr (ZERO_SKIP) skip_a = __all(d.zrow == (1u << NR) - 1);
         if (!skip_a) layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
+        stamp(a, 3);
         if constexpr (T > 4) {
             Stager<T, (LateS2<P, T>::value ? G::NTAB : 0)> s2;
-            if constexpr (LateS2<P, T>::value) s2.issue(a, TwiddleEntry<T>{a, c, 0, a.skew_fft});
+            if constexpr (LateS2<P, T>::value) s2.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
             exchange<T, NQR, false>(L, H, c, lds, [&]() {
                 if constexpr (LateS2<P, T>::value) s2.commit((uint4*)(smem + SM::TAB2_OFF));
             });
+            stamp(a, 4);
             layers<T, true, 4, (T > 4 ? T : 4), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
                                                                                                 tab2, d.zmask);
             in_b = true;
         }
+        stamp(a, 5);
     }
     // ---------------- formal derivative (tile bits) ----------------
     if constexpr (PT::FD) {
         if (in_b) tile_fd<T, NQR, true>(L, H, L, H, c, lds);
         else tile_fd<T, NQR, false>(L, H, L, H, c, lds);
+        stamp(a, 6);
     }
     // ---------------- FFT ----------------
     if constexpr (PT::FFT) {
         if constexpr (T > 4) {
             layers<T, true, 4, (T > 4 ? T : 4), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
+            stamp(a, 7);
             exchange<T, NQR, true>(L, H, c, lds);
+            stamp(a, 8);
             in_b = false;
         }
         bool need = true;
         if constexpr (P == DEC_MID) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
         if (need) layers<T, false, 0, R, true, TWO>(L, H, c, a, tab1, tab2);
+        stamp(a, 9);
     }
 
     // ---------------- store ----------------
@@ -860,18 +902,23 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         const uint32_t k = kidx<T, END_B>(c, m);
         const uint32_t r = row_rel<T>(cs, a, k);
         if constexpr (PT::STORE == ST_PLAIN) {
-            st_quad(a, a.out + (uint64_t)r * a.S, P != DEC_MID || (k >= a.need_lo && k < a.need_hi), cs, L[m], H[m]);
+            st_quad(a, a.out + (uint64_t)r * a.S_out, P != DEC_MID || (k >= a.need_lo && k < a.need_hi), cs, L[m], H[m]);
         } else if constexpr (PT::STORE == ST_RECOVERY) {
-            st_quad(a, a.out + (uint64_t)r * a.S, r < a.out_rows, cs, L[m], H[m]);
+            st_quad(a, a.out + (uint64_t)r * a.S_out, r < a.out_rows, cs, L[m], H[m]);
         } else {
             uint32_t tt[20];
             load_table_lds(tt, rvt + k * 5);
             uint32_t ol = 0, oh = 0;
             mul_xor(ol, oh, L[m], H[m], tt);
             const uint32_t i = r + a.row_base_out - (a.rest_seg_b ? a.chunk : 0);
-            st_quad(a, a.rest + (uint64_t)i * a.S, lostf[k] != 0, cs, ol, oh);
+            st_quad(a, a.rest + (uint64_t)i * a.S_rest, lostf[k] != 0, cs, ol, oh);
         }
     }
+    stamp(a, 10);
+#if RS16_STAMPS
+    __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
+    stamp(a, 11);
+#endif
 }
 
 // The persistent pass: workgroup b processes items [b * per_wg, ...) of the
@@ -903,11 +950,17 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
 #if !RS16_PIPE
     // one item per workgroup (launch_pass sets per_wg = 1): straight-line code
     // (a loop lets the compiler hoist per-row address terms out of it, which
-    // costs more VGPRs than the 128 of four waves per SIMD).  The tile's
-    // loads are issued first, so the table staging overlaps their latency.
+    // costs more VGPRs than the 128 of four waves per SIMD).  The twiddle
+    // tables are requested first, the tile's rows right behind them, so the
+    // staging latency hides under the row loads.
+    stamp(a, 0);
+    TileStage<P, T> st;
+    st.issue(a, c);  // twiddle tables first: they do not queue behind the tile
     ItemRegs<P, T> cur;
     load_item<P, T>(a, c, tile, cur);
-    stage_tile<P, T>(a, c, tile, smem);
+    stamp(a, 1);
+    st.finish(a, c, smem);
+    stamp(a, 2);
     process_item<P, T>(a, c, tile, slab, cur, smem);
 #else
     stage_tile<P, T>(a, c, tile, smem);

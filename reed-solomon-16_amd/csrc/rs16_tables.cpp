@@ -8,6 +8,7 @@
 //   LogWalsh = FWHT(log) with log[0] = 0 (src/engine/tables.rs:127-139).
 // The device-side multiply tables are a GPU-specific format (v_perm byte
 // tables, rs16_gf.hpp), not the reference's Mul16 nibble tables.
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -109,6 +110,12 @@ void build(HostTables& t) {
             }
     }
     // entry ZERO_ENTRY stays all zero.
+
+    // The table of every twiddle index, so that a pass stages a twiddle's
+    // table with one load instead of skew_entry -> mul_tab.
+    t.skew_tab.resize((size_t)GF_ORDER * TAB_DWORDS);
+    for (uint32_t i = 0; i < GF_ORDER; i++)
+        std::copy_n(&t.mul_tab[(size_t)t.skew_entry[i] * TAB_DWORDS], TAB_DWORDS, &t.skew_tab[(size_t)i * TAB_DWORDS]);
 }
 }  // namespace
 

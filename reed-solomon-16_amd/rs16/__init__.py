@@ -169,6 +169,10 @@ class Engine:
     def synchronize(self, stream=None):
         _check(lib().rs16_engine_synchronize(self.h, stream, C.byref(self._err)), self._err)
 
+    def set_slices(self, n: int):
+        """Concurrent column slices of the device one-shot codec (1..4)."""
+        _check(lib().rs16_engine_set_slices(self.h, n, C.byref(self._err)), self._err)
+
     def create_stream(self) -> int:
         """A new non-blocking hipStream_t on this engine's device (raw handle)."""
         p = lib().rs16_stream_create(self.h, C.byref(self._err))

@@ -31,6 +31,8 @@ SIGNATURES = {
     "rs16_engine_profile_reset": (None, [_p]),
     "rs16_prog_count": (_i, []),
     "rs16_prog_name": (C.c_char_p, [_i]),
+    "rs16_engine_set_stamps": (_i, [_p, _p, _i, _e]),
+    "rs16_engine_set_slices": (_i, [_p, _i, _e]),
     "rs16_engine_new": (_p, [_i, _e]),
     "rs16_engine_free": (None, [_p]),
     "rs16_engine_device": (_i, [_p]),

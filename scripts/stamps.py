@@ -1,0 +1,87 @@
+"""Phase timeline of the pass kernels (diagnostic; needs a -DRS16_STAMPS=1
+library, e.g. RS16_LIB=reed-solomon-16_amd/build_stamps/librs16.so).
+
+Runs the bench's step (32768:32768 x 1 KiB encode + 100 %-loss decode) with
+the stamps of one pass program at a time and prints, per pass: the spread
+of workgroup start / end times (s_memrealtime, 100 MHz) and the median
+duration of each phase of a workgroup (s_memtime cycles at the workgroup's
+own clock).  Phases (rs16_pass.hip stamp()): 0 start, 1 loads issued,
+2 tables staged, 3 first layout-A layers, 4 layout switch, 5 first
+direction done, 6 formal derivative, 7 layout-B FFT layers, 8 layout
+switch, 9 last layers, 10 stores issued, 11 stores done."""
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "reed-solomon-16_amd"))
+import rs16  # noqa: E402
+from rs16._lib import RS16Error, lib  # noqa: E402
+from rs16.device import DeviceArray  # noqa: E402
+from rs16.util import generate_original  # noqa: E402
+
+PH = ["start", "loads", "staged", "A-layers", "switch1", "dir1", "fd", "B-fft", "switch2", "last", "stores", "drain"]
+
+
+def main():
+    k = m = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
+    S = 1024
+    eng = rs16.Engine(0)
+    original = generate_original(k, S, 0)
+    d_orig = DeviceArray.from_numpy(eng, original)
+    d_rec = DeviceArray(eng, m * S)
+    d_rest = DeviceArray(eng, k * S)
+    d_of = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+    d_rf = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+
+    def step():
+        rs16.encode_device(k, m, S, d_orig.ptr, d_rec.ptr, engine=eng)
+        rs16.decode_device(k, m, S, d_rest.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, 0, m, engine=eng)
+
+    for _ in range(3):
+        step()
+    eng.synchronize()
+    assert np.array_equal(d_rest.download(shape=(k, S)), original)
+    names = {lib().rs16_prog_name(i).decode(): i for i in range(lib().rs16_prog_count())}
+    nwg = 8192
+    buf = DeviceArray(eng, nwg * 16 * 8)
+    err = RS16Error()
+    out = {}
+    for name in ["ENC_FIRST", "ENC_MID", "ENC_LAST", "DEC_HALF_FIRST", "DEC_HALF_MID", "DEC_HALF_LAST"]:
+        buf.upload(np.zeros(nwg * 16, np.uint64))
+        lib().rs16_engine_set_stamps(eng.h, buf.ptr, names[name], C.byref(err))
+        step()
+        eng.synchronize()
+        lib().rs16_engine_set_stamps(eng.h, None, -1, C.byref(err))
+        st = buf.download(np.uint64).reshape(nwg, 16).astype(np.int64)
+        st = st[st[:, 0] != 0]
+        if len(st) == 0:
+            continue
+        rt0 = st[:, 14].min()
+        start_us = (st[:, 14] - rt0) / 100.0
+        end_us = (st[:, 15] - rt0) / 100.0
+        ghz = (st[:, 11] - st[:, 0]) / np.maximum(st[:, 15] - st[:, 14], 1) / 100.0 * 1e-0 * 100 / 100
+        ghz = (st[:, 11] - st[:, 0]) / np.maximum((st[:, 15] - st[:, 14]) * 10.0, 1)  # cycles per ns
+        rec = [p for p in range(12) if (st[:, p] != 0).all()]
+        phases = {}
+        for a, b in zip(rec, rec[1:]):
+            dur = (st[:, b] - st[:, a]) / ghz / 1000.0  # us
+            phases[f"{PH[a]}->{PH[b]}"] = round(float(np.median(dur)), 2)
+        out[name] = {
+            "workgroups": int(len(st)),
+            "clock_ghz_median": round(float(np.median(ghz)), 3),
+            "start_spread_us": round(float(start_us.max()), 2),
+            "end_min_max_us": [round(float(end_us.min()), 2), round(float(end_us.max()), 2)],
+            "lifetime_median_us": round(float(np.median(end_us - start_us)), 2),
+            "phase_median_us": phases,
+        }
+        print(name, json.dumps(out[name]), flush=True)
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / "stamps.json").write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -187,3 +187,27 @@ def test_configs4_per_gpu_column_slice(eng):
     om = np.zeros(k, bool)
     rm = np.ones(m, bool)
     assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+
+
+@pytest.mark.parametrize("slices", [1, 2, 3, 4])
+@pytest.mark.parametrize("k,m,sb", [(1000, 1000, 192), (3000, 3000, 1024), (100, 200, 320)])
+def test_column_slices(eng, slices, k, m, sb):
+    # the device one-shot codec split into concurrent column slices
+    # (rs16_engine_set_slices): identical results for any slice count,
+    # including widths that do not divide evenly into 64-byte blocks
+    eng.set_slices(slices)
+    try:
+        original = generate_original(k, sb, slices)
+        recovery = dev_encode(eng, original, m)
+        assert np.array_equal(recovery, O.encode(k, m, original))
+        om = np.zeros(k, bool)
+        om[: k // 3] = True
+        rm = np.zeros(m, bool)
+        rm[: k - k // 3] = True
+        assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+        om[:] = False
+        rm[:] = False
+        rm[m - k:] = True  # 100 % loss: the half-transform path
+        assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+    finally:
+        eng.set_slices(1)
