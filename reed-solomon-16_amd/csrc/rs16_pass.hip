@@ -93,13 +93,18 @@ RS16_PROG(DEC_HALF_SINGLE, LD_GATHER_DEC, true, false, true, ST_RESTORE)
 #ifndef RS16_PIPE
 #define RS16_PIPE 0
 #endif
+// Quads per tile row at T = 8 in the one-item build: 32 (8-wave workgroups,
+// two per CU) or 16 (4-wave workgroups, four per CU).
+#ifndef RS16_Q8
+#define RS16_Q8 32
+#endif
 template <int T> struct Geo {
     static constexpr int R = T > 4 ? 4 : T;               // row bits held in registers
     static constexpr int NR = 1 << R;                     // rows per thread (a row set)
     static constexpr int SETS = 1 << (T - R);             // row sets per tile
     // quads per tile row: PIPE: 4 waves per workgroup from T = 6 on
     // (Q = 256 / SETS); else 32 (two 16-row sets per wave) from T = 5 on
-    static constexpr int Q = (RS16_PIPE && T >= 6) ? 256 / SETS : (T > 4 ? 32 : 64);
+    static constexpr int Q = (RS16_PIPE && T >= 6) ? 256 / SETS : (T == 8 ? RS16_Q8 : (T > 4 ? 32 : 64));
     static constexpr int HWS = 64 / Q;                    // row sets per wave
     static constexpr int W = SETS / HWS > 0 ? SETS / HWS : 1;  // waves per workgroup
     static constexpr int SHB = T - R;                     // layout B: k = s + (m << SHB)
@@ -131,7 +136,11 @@ template <int P, int T> struct Smem {
     static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
     static constexpr int ERT_OFF = IMG_BYTES;
     static constexpr int TAB1_BYTES = Geo<T>::NTAB * 80;
-    static constexpr int TAB2_BYTES = TWO ? Geo<T>::NTAB * 80 : 0;
+    // Restage (one-item build, T > 4): tab2 holds only the second
+    // direction's layout-B tables; its layout-A tables are written over the
+    // first direction's in tab1 at the first layout switch.
+    static constexpr bool RESTAGE = TWO && T > 4 && !RS16_PIPE;
+    static constexpr int TAB2_BYTES = TWO ? (RESTAGE ? Geo<T>::NTAB - Geo<T>::TSPLIT : Geo<T>::NTAB) * 80 : 0;
     static constexpr int RVT_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 80 : 0;
     static constexpr int LOST_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 4 : 0;
     static constexpr int TAB1_OFF = ERT_OFF + ERT_BYTES;
@@ -370,6 +379,28 @@ template <int NT> __device__ __forceinline__ void fwht256_tile(uint32_t* s) {
     }
     __syncthreads();
 }
+// The same 256-point FWHT by one wave in registers: lane l holds
+// v[j] = x[l + 64 j]; distances 1..32 are lane pairs (shuffles), 64 and 128
+// register pairs.  Residues equal fwht256_tile's (every consumer of these
+// logs treats 65535 and 0 alike, exp[65535] == exp[0]).
+__device__ __forceinline__ void fwht256_wave(uint32_t (&v)[4]) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const bool hi = lane & d;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t p = (uint32_t)__shfl_xor((int)v[j], d);
+            v[j] = hi ? sub_mod(p, v[j]) : add_mod(v[j], p);
+        }
+    }
+    uint32_t a = add_mod(v[0], v[1]), b = sub_mod(v[0], v[1]);
+    uint32_t c = add_mod(v[2], v[3]), e = sub_mod(v[2], v[3]);
+    v[0] = add_mod(a, c);
+    v[2] = sub_mod(a, c);
+    v[1] = add_mod(b, e);
+    v[3] = sub_mod(b, e);
+}
 
 // Layers for k-bits [KB0, KB1) held in registers of layout LB, as a
 // compile-time sequence of twiddle groups (step s, index gi).
@@ -408,7 +439,10 @@ __device__ __forceinline__ const uint4* group_table(const Thr& c, const uint4* t
     // layout A: k = (s << R) + m  ->  j = (s << (R-1-kb)) + gi ; layout B: j = gi
     const uint32_t j = LB ? (uint32_t)gi : (c.s << (Geo<T>::R - 1 - kb)) + gi;
     const uint32_t t = off + j;
-    return (IN_TAB2 ? tab2 : tab1) + t * 5;
+    // tab2 starts at the first layout-B table when the layout-A ones are
+    // restaged into tab1 (Smem::RESTAGE); T <= 4 has no layout B (TSPLIT = 0)
+    constexpr uint32_t base2 = (!RS16_PIPE && T > 4) ? Geo<T>::TSPLIT : 0;
+    return IN_TAB2 ? tab2 + (t - base2) * 5 : tab1 + t * 5;
 }
 
 // Empty volatile asm that "redefines" the data registers: ALU work cannot
@@ -598,12 +632,12 @@ __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H
     }
 }
 
-// Two-direction programs of the one-item-per-workgroup build stage the
-// second direction's tables during the first direction (issued before the
-// first layout switch, written to LDS between its barriers), so that their
-// staging registers are not live together with the first direction's.
+// Two-direction programs of the one-item build (Smem::RESTAGE): the second
+// direction's layout-A tables are requested before the first layout switch
+// and written over the first direction's layout-A tables (dead by then) in
+// tab1 between its barriers.
 template <int P, int T> struct LateS2 {
-    static constexpr bool value = ProgTraits<P>::IFFT && ProgTraits<P>::FFT && T > 4 && !RS16_PIPE;
+    static constexpr bool value = Smem<P, T>::RESTAGE;
 };
 
 // y = x + (in-tile formal derivative part) of the rows in registers, where
@@ -743,30 +777,81 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
 // per-row multipliers, writes everything to LDS and ends with a barrier.  The
 // caller must have a barrier between the previous key's last use of these
 // LDS regions and finish().
+// Reveal multipliers (65535 - e of the lost originals) and lost-row flags of
+// the tile; programs with a last layout switch stage them there
+// (LateReveal), off the load phase -- they are read only by the stores.
+template <int P, int T> struct LateReveal {
+    static constexpr bool value = ProgTraits<P>::STORE == ST_RESTORE && ProgTraits<P>::FFT && T > 4;
+};
+template <int P, int T> struct RevealStage {
+    using SM = Smem<P, T>;
+    using G = Geo<T>;
+    Stager<T, (1 << T)> sr;
+    uint32_t lost[((1 << T) + G::THREADS - 1) / G::THREADS];
+    __device__ __forceinline__ void issue(const PassArgs& a, const Thr& c, const uint32_t* el) {
+        sr.issue(a.mul_tab, RevealEntry<T>{a, c, el});
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof lost / sizeof lost[0]); i++) {
+            const uint32_t k = threadIdx.x + i * G::THREADS;
+            lost[i] = k < (1u << T) && row_lost_original(a, row_rel<T>(c, a, k) + a.row_base_out);
+        }
+    }
+    __device__ __forceinline__ void commit(const PassArgs& a, const Thr& c, uint8_t* smem) const {
+        (void)a;
+        (void)c;
+        uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof lost / sizeof lost[0]); i++) {
+            const uint32_t k = threadIdx.x + i * G::THREADS;
+            if (k < (1u << T)) lostf[k] = lost[i];
+        }
+        sr.commit((uint4*)(smem + SM::RVT_OFF));
+    }
+};
+
 template <int P, int T> struct TileStage {
     using PT = ProgTraits<P>;
     using SM = Smem<P, T>;
     using G = Geo<T>;
-    static constexpr bool S2 = SM::TWO && !LateS2<P, T>::value;
+    // second direction at the start: all of it, or only its layout-B tables
+    static constexpr int N2 = !SM::TWO ? 0 : (LateS2<P, T>::value ? G::NTAB - G::TSPLIT : G::NTAB);
+    static constexpr bool S2 = N2 > 0;
     Stager<T, G::NTAB> s1;
-    Stager<T, (S2 ? G::NTAB : 0)> s2;
+    Stager<T, N2> s2;
 
+    uint32_t ev[4];  // wave 0: the tile's 256-row block of eval_poly's work (ework)
+
+    // the 256-row block holding the tile's decode rows (contiguous tiles of
+    // 2^T <= 256 rows at a multiple of 2^T lie in one block)
+    __device__ __forceinline__ uint32_t elog_row0(const PassArgs& a, const Thr& c) const {
+        const uint32_t base = PT::LOAD == LD_GATHER_DEC ? a.row_base_in : a.row_base_out;
+        return row_rel<T>(c, a, 0) + base;
+    }
     __device__ __forceinline__ void issue(const PassArgs& a, const Thr& c) {
+        if constexpr (SM::ELOG_BYTES > 0) {
+            // requested first: the erasure logs head the staging chain
+            if (a.ework && c.w == 0) {
+                const uint32_t* src = a.ework + (elog_row0(a, c) & ~255u) + c.lane;
+#pragma unroll
+                for (int j = 0; j < 4; j++) ev[j] = src[64 * j];
+            }
+        }
         s1.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
-        if constexpr (S2) s2.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
+        if constexpr (S2) s2.issue(a.skew_tab, TwiddleEntry<T>{a, c, G::NTAB - N2, a.skew_fft});
     }
     __device__ __forceinline__ void finish(const PassArgs& a, const Thr& c, uint8_t* smem) {
         const uint32_t* el = nullptr;
         if constexpr (SM::ELOG_BYTES > 0) {
             if (a.ework) {
-                // the 256-row block holding the tile's decode rows (contiguous
-                // tiles of 2^T <= 256 rows at a multiple of 2^T lie in one block)
-                const uint32_t base = PT::LOAD == LD_GATHER_DEC ? a.row_base_in : a.row_base_out;
-                const uint32_t row0 = row_rel<T>(c, a, 0) + base;
+                // the last 256-point FWHT of eval_poly, by wave 0 in registers
                 uint32_t* elds = (uint32_t*)(smem + SM::ELOG_OFF);
-                for (uint32_t i = threadIdx.x; i < 256; i += G::THREADS) elds[i] = a.ework[(row0 & ~255u) + i];
-                fwht256_tile<G::THREADS>(elds);
-                el = elds + (row0 & 255u);
+                if (c.w == 0) {
+                    fwht256_wave(ev);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) elds[c.lane + 64 * j] = ev[j];
+                }
+                __syncthreads();
+                el = elds + (elog_row0(a, c) & 255u);
             }
         }
         if constexpr (PT::LOAD == LD_GATHER_DEC) {
@@ -774,13 +859,10 @@ template <int P, int T> struct TileStage {
             se.issue(a.mul_tab, GatherEntry<T>{a, c, el});
             se.commit((uint4*)(smem + SM::ERT_OFF));
         }
-        if constexpr (PT::STORE == ST_RESTORE) {
-            Stager<T, (1 << T)> sr;
-            sr.issue(a.mul_tab, RevealEntry<T>{a, c, el});
-            uint32_t* lostf = (uint32_t*)(smem + SM::LOST_OFF);
-            for (uint32_t k = threadIdx.x; k < (1u << T); k += G::THREADS)
-                lostf[k] = row_lost_original(a, row_rel<T>(c, a, k) + a.row_base_out);
-            sr.commit((uint4*)(smem + SM::RVT_OFF));
+        if constexpr (PT::STORE == ST_RESTORE && !LateReveal<P, T>::value) {
+            RevealStage<P, T> rs;
+            rs.issue(a, c, el);
+            rs.commit(a, c, smem);
         }
         if constexpr (S2) s2.commit((uint4*)(smem + SM::TAB2_OFF));
         s1.commit((uint4*)(smem + SM::TAB1_OFF));
@@ -851,10 +933,10 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         if (!skip_a) layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
         stamp(a, 3);
         if constexpr (T > 4) {
-            Stager<T, (LateS2<P, T>::value ? G::NTAB : 0)> s2;
-            if constexpr (LateS2<P, T>::value) s2.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
+            Stager<T, (LateS2<P, T>::value ? G::TSPLIT : 0)> s3;
+            if constexpr (LateS2<P, T>::value) s3.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
             exchange<T, NQR, false>(L, H, c, lds, [&]() {
-                if constexpr (LateS2<P, T>::value) s2.commit((uint4*)(smem + SM::TAB2_OFF));
+                if constexpr (LateS2<P, T>::value) s3.commit((uint4*)(smem + SM::TAB1_OFF));
             });
             stamp(a, 4);
             layers<T, true, 4, (T > 4 ? T : 4), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
@@ -875,13 +957,27 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             layers<T, true, 4, (T > 4 ? T : 4), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
             stamp(a, 7);
-            exchange<T, NQR, true>(L, H, c, lds);
+            // reveal multipliers: requested before the last layout switch,
+            // written to LDS between its barriers (read after the layers)
+            RevealStage<P, (LateReveal<P, T>::value ? T : 0)> rs;
+            if constexpr (LateReveal<P, T>::value) {
+                const uint32_t* el = nullptr;
+                if (a.ework) {
+                    const uint32_t base = a.row_base_out;
+                    el = (const uint32_t*)(smem + SM::ELOG_OFF) + ((row_rel<T>(c, a, 0) + base) & 255u);
+                }
+                rs.issue(a, c, el);
+            }
+            exchange<T, NQR, true>(L, H, c, lds, [&]() {
+                if constexpr (LateReveal<P, T>::value) rs.commit(a, c, smem);
+            });
             stamp(a, 8);
             in_b = false;
         }
         bool need = true;
         if constexpr (P == DEC_MID) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
-        if (need) layers<T, false, 0, R, true, TWO>(L, H, c, a, tab1, tab2);
+        // second direction's layout-A tables: restaged into tab1 (T > 4), else in tab2
+        if (need) layers<T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2);
         stamp(a, 9);
     }
 
