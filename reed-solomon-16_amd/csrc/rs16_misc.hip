@@ -172,25 +172,80 @@ __global__ void __launch_bounds__(256) fwht_lo_kernel(const uint32_t* in32, cons
     else out32[idx] = s[threadIdx.x];
 }
 
-// Contiguous 256-point FWHT of the erasure vector built from the received flags.
-__global__ void __launch_bounds__(256) fwht_lo_flags_kernel(ErasureSpec e, uint32_t* out32) {
-    __shared__ uint32_t s[256];
-    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
-    if (blockIdx.x * 256u < e.n) decode_flags_block(e, blockIdx.x * 256u);
-    s[threadIdx.x] = erasure_at(e, idx);
-    fwht256_lds(s);
-    out32[idx] = s[threadIdx.x];
+// 256-point FWHT in Z/65535 by one wave in registers: lane l holds
+// v[j] = x[l + 64 j]; distances 1..32 are lane pairs (shuffles), 64 and 128
+// register pairs.  No barriers.  (Residues as fwht256_lds; consumers of the
+// decode's erasure logs treat 65535 and 0 alike, exp[65535] == exp[0].)
+__device__ __forceinline__ void fwht256_wave(uint32_t (&v)[4]) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const bool hi = lane & d;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t p = (uint32_t)__shfl_xor((int)v[j], d);
+            v[j] = hi ? sub_mod(p, v[j]) : add_mod(v[j], p);
+        }
+    }
+    const uint32_t a = add_mod(v[0], v[1]), b = sub_mod(v[0], v[1]);
+    const uint32_t c = add_mod(v[2], v[3]), d = sub_mod(v[2], v[3]);
+    v[0] = add_mod(a, c);
+    v[2] = sub_mod(a, c);
+    v[1] = add_mod(b, d);
+    v[3] = sub_mod(b, d);
 }
-// Strided 256-point FWHT (row bits 8-15), x LogWalsh mod 65535, and again.
-__global__ void __launch_bounds__(256) fwht_hi_mulw_kernel(const uint32_t* in32, uint32_t* out32,
-                                                           const uint16_t* log_walsh) {
-    __shared__ uint32_t s[256];
-    const uint32_t idx = blockIdx.x + 256u * threadIdx.x;
-    s[threadIdx.x] = in32[idx];
-    fwht256_lds(s);
-    s[threadIdx.x] = (uint32_t)(((uint64_t)s[threadIdx.x] * log_walsh[idx]) % GF_MODULUS);
-    fwht256_lds(s);
-    out32[idx] = s[threadIdx.x];
+
+// Contiguous 256-point FWHT of the erasure vector built from the received
+// flags, one wave per 256-row block; the same wave writes the block's
+// received bitmap (ballots) and zero-tile flags.
+__global__ void __launch_bounds__(64) fwht_lo_flags_kernel(ErasureSpec e, uint32_t* out32) {
+    const uint32_t base = blockIdx.x * 256u, lane = threadIdx.x;
+    uint32_t v[4];
+    uint64_t rmask[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t i = base + lane + 64u * j;
+        v[j] = erasure_at(e, i);
+        rmask[j] = __ballot(i < e.n && received_at(e, i));
+    }
+    if (base < e.n) {
+        if (e.rbits && lane < 8 && base + 32u * lane < e.n)
+            e.rbits[(base >> 5) + lane] = (uint32_t)(rmask[lane >> 1] >> (32 * (lane & 1)));
+        if (e.zflags) {
+            const uint32_t ts = 1u << e.zlo, ntile = e.n >> e.zlo;
+            // tile t of this block: rows [t ts, (t + 1) ts), t < 256 / ts
+            for (uint32_t t = lane; t < 256u / ts; t += 64) {
+                bool any = false;
+                for (uint32_t r = t * ts; r < (t + 1) * ts; r += 64) {
+                    const uint32_t w = r >> 6, sh = r & 63, len = ts < 64 ? ts : 64;
+                    const uint64_t m = len == 64 ? ~0ull : ((1ull << len) - 1) << sh;
+                    any |= (rmask[w] & m) != 0;
+                }
+                if ((base >> e.zlo) + t < ntile) e.zflags[(base >> e.zlo) + t] = any ? 0 : 1;
+            }
+        }
+    }
+    fwht256_wave(v);
+#pragma unroll
+    for (int j = 0; j < 4; j++) out32[base + lane + 64u * j] = v[j];
+}
+// Strided 256-point FWHT (row bits 8-15), x LogWalsh mod 65535, and again;
+// one wave per column.
+__global__ void __launch_bounds__(64) fwht_hi_mulw_kernel(const uint32_t* in32, uint32_t* out32,
+                                                          const uint16_t* log_walsh) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = in32[blockIdx.x + 256u * (lane + 64u * j)];
+    fwht256_wave(v);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t idx = blockIdx.x + 256u * (lane + 64u * j);
+        v[j] = (uint32_t)(((uint64_t)v[j] * log_walsh[idx]) % GF_MODULUS);
+    }
+    fwht256_wave(v);
+#pragma unroll
+    for (int j = 0; j < 4; j++) out32[blockIdx.x + 256u * (lane + 64u * j)] = v[j];
 }
 
 // eval_poly(e) = FWHT(LogWalsh . FWHT(e)) with FWHT = H_lo H_hi (row bits 0-7
@@ -200,8 +255,8 @@ __global__ void __launch_bounds__(256) fwht_hi_mulw_kernel(const uint32_t* in32,
 // finish it per tile in LDS (rs16_pass.hip), saving a kernel.
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
-    hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(256), 0, s, e, work);
-    hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(256), 0, s, work, work, log_walsh);
+    hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(64), 0, s, e, work);
+    hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(64), 0, s, work, work, log_walsh);
     if (last_lo)
         hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
                            nullptr);

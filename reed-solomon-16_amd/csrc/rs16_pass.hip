@@ -190,6 +190,34 @@ template <int T> __device__ __forceinline__ uint32_t row_rel(const Thr& c, const
 #ifndef RS16_STAMPS
 #define RS16_STAMPS 0
 #endif
+// Priority schedule: a wave lowers its issue priority (s_setprio 3 -> 0) as
+// its item progresses, so that waves that are behind win the arbitration.
+// Hardware age order alone lets the oldest workgroup of a CU run ahead and
+// leaves a low-occupancy one-workgroup tail (scripts/stamps.py: 10-16 us
+// spread of workgroup end times).  Measured (bench, 2 runs each): 1 = all
+// passes 620 / 614 GiB/s, 2 = two-direction passes only 611 / 611, 3 = a
+// later schedule 607, 0 = off 595 / 594.
+#ifndef RS16_PRIO
+#define RS16_PRIO 1
+#endif
+// at point `at` of program P's item (0 staged, 1 first layout-A layers done,
+// 2 first direction done, 3 layout-B FFT done, 4 last switch done, 5 stores)
+template <int P, int at> __device__ __forceinline__ void prio() {
+#if RS16_PRIO
+    constexpr bool two = ProgTraits<P>::IFFT && ProgTraits<P>::FFT;
+    if constexpr (RS16_PRIO == 1) {
+        constexpr int v[6] = {3, 2, -1, 1, -1, 0};
+        if constexpr (v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
+    } else if constexpr (RS16_PRIO == 2) {
+        constexpr int v[6] = {3, 2, -1, 1, -1, 0};
+        if constexpr (two && v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
+    } else {
+        constexpr int v[6] = {3, -1, 2, -1, 1, 0};
+        if constexpr (two && v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
+    }
+#endif
+}
+
 __device__ __forceinline__ void stamp(const PassArgs& a, int i) {
 #if RS16_STAMPS
     if (a.stamps && threadIdx.x == 0) {
@@ -932,6 +960,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         if constexpr (ZERO_SKIP) skip_a = __all(d.zrow == (1u << NR) - 1);
         if (!skip_a) layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
         stamp(a, 3);
+        prio<P, 1>();
         if constexpr (T > 4) {
             Stager<T, (LateS2<P, T>::value ? G::TSPLIT : 0)> s3;
             if constexpr (LateS2<P, T>::value) s3.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
@@ -944,6 +973,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             in_b = true;
         }
         stamp(a, 5);
+        prio<P, 2>();
     }
     // ---------------- formal derivative (tile bits) ----------------
     if constexpr (PT::FD) {
@@ -957,6 +987,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             layers<T, true, 4, (T > 4 ? T : 4), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
             stamp(a, 7);
+            prio<P, 3>();
             // reveal multipliers: requested before the last layout switch,
             // written to LDS between its barriers (read after the layers)
             RevealStage<P, (LateReveal<P, T>::value ? T : 0)> rs;
@@ -972,6 +1003,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                 if constexpr (LateReveal<P, T>::value) rs.commit(a, c, smem);
             });
             stamp(a, 8);
+            prio<P, 4>();
             in_b = false;
         }
         bool need = true;
@@ -981,6 +1013,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         stamp(a, 9);
     }
 
+    prio<P, 5>();
     // ---------------- store ----------------
     // The next item's loads were issued before this item's butterflies and
     // have landed by now: retire them before the stores, so that the stores
@@ -1055,6 +1088,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     ItemRegs<P, T> cur;
     load_item<P, T>(a, c, tile, cur);
     stamp(a, 1);
+    prio<P, 0>();
     st.finish(a, c, smem);
     stamp(a, 2);
     process_item<P, T>(a, c, tile, slab, cur, smem);
