@@ -704,8 +704,24 @@ template <int P, int T> struct ItemRegs {
 // Per-item coordinates of this thread: item -> (tile, slab).
 __device__ __forceinline__ void set_item(Thr& c, const PassArgs& a, uint32_t item, uint32_t Q, uint32_t& tile,
                                          uint32_t& slab) {
+#if !RS16_PIPE
+    // One item per workgroup, XCD-aware: workgroups are dealt to the 8 XCDs
+    // round-robin (XCD = block mod 8, speed only), so with a tile count that
+    // is a multiple of 8 all slabs of a tile run on one XCD (they share the
+    // tile's twiddle tables in its L2) and consecutive tiles go to different
+    // XCDs (tiles of uneven work spread evenly).
+    if ((a.ntiles & 7) == 0) {
+        const uint32_t i = item >> 3;
+        slab = i % a.nslab;
+        tile = (i / a.nslab) * 8 + (item & 7);
+    } else {
+        tile = item / a.nslab;
+        slab = item - tile * a.nslab;
+    }
+#else
     tile = item / a.nslab;
     slab = item - tile * a.nslab;
+#endif
     tile += a.tile_base;
     c.b_low = tile & ((1u << a.lo) - 1);
     c.b_high = tile >> a.lo;
