@@ -63,6 +63,15 @@ typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 enum LoadMode { LD_PLAIN = 0, LD_GATHER_ENC, LD_GATHER_DEC, LD_DEC_LAST };
 enum StoreMode { ST_PLAIN = 0, ST_RECOVERY, ST_RESTORE };
 
+// Store cache policy (RS16_STPOL): 0 plain, 1 nt on the single-direction
+// passes, 4 nt everywhere, 2 sc1 (agent scope: the line leaves the XCD's L2
+// at once), 3 sc0 sc1 (system scope).  Load policy (RS16_LDPOL): 0 plain, 1 nt.
+#ifndef RS16_STPOL
+#define RS16_STPOL 1
+#endif
+#ifndef RS16_LDPOL
+#define RS16_LDPOL 0
+#endif
 template <int P> struct ProgTraits;
 #define RS16_PROG(P, LD, I, F, FF, ST)          \
     template <> struct ProgTraits<P> {         \
@@ -71,6 +80,8 @@ template <int P> struct ProgTraits;
         static constexpr bool FD = F;          \
         static constexpr bool FFT = FF;        \
         static constexpr int STORE = ST;       \
+        static constexpr bool ST_NT = RS16_STPOL == 4 || (RS16_STPOL == 1 && !(I && FF)) || \
+                                      (RS16_STPOL == 5 && ST != ST_PLAIN);                  \
     };
 RS16_PROG(GEN_FFT, LD_PLAIN, false, false, true, ST_PLAIN)
 RS16_PROG(GEN_IFFT, LD_PLAIN, true, false, false, ST_PLAIN)
@@ -186,7 +197,8 @@ template <int T> __device__ __forceinline__ uint32_t row_rel(const Thr& c, const
 // Diagnostic timeline build (-DRS16_STAMPS=1, never the shipped library):
 // wave 0 of every workgroup stores s_memtime at phase boundaries to
 // stamps[block * 16 + phase] (phase 15: s_memrealtime at the end, 14 at
-// the start, for the clock).  scripts/stamps.py reads them.
+// the start, for the clock; 12 / 13 the HW_ID / XCC_ID registers).
+// scripts/stamps.py reads them.
 #ifndef RS16_STAMPS
 #define RS16_STAMPS 0
 #endif
@@ -222,7 +234,12 @@ __device__ __forceinline__ void stamp(const PassArgs& a, int i) {
 #if RS16_STAMPS
     if (a.stamps && threadIdx.x == 0) {
         a.stamps[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
-        if (i == 0) a.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+        if (i == 0) {
+            a.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+            // slots 12 / 13: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
+            a.stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            a.stamps[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        }
         if (i == 11) a.stamps[blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memrealtime();
     }
 #else
@@ -235,6 +252,21 @@ __device__ __forceinline__ void stamp(const PassArgs& a, int i) {
 // (expcnt and lgkmcnt at their maxima, i.e. not waited for).
 __host__ __device__ constexpr int vmcnt_wait(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
+template <bool NT> __device__ __forceinline__ void st_dword(uint32_t* p, uint32_t v) {
+    if constexpr (NT) {
+        __builtin_nontemporal_store(v, p);
+    } else if constexpr (RS16_STPOL == 2) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (RS16_STPOL == 3) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        *p = v;
+    }
+}
+__device__ __forceinline__ uint32_t ld_dword(const uint32_t* p) {
+    if constexpr (RS16_LDPOL == 1) return __builtin_nontemporal_load(p);
+    return *p;
+}
 // Quad loads / stores.  In the pipelined build they have no control flow: a
 // row that is not read (ok = false, or a lane past the row end) comes from
 // the zero page, a row that is not written goes to the sink (PassArgs::zero /
@@ -255,14 +287,15 @@ __device__ __forceinline__ void ld_quad(const PassArgs& a, const uint8_t* row, b
     L = H = 0;
     if (ok && c.active) {
         const uint32_t* p = (const uint32_t*)(row + c.offL);
-        L = p[0];
-        H = p[8];
+        L = ld_dword(p);
+        H = ld_dword(p + 8);
     }
 #endif
 }
 // A dropped store: in the pipelined build it goes to the sink (2 KiB per
 // workgroup slot, so that workgroups do not all write the same lines); the
 // one-item build, which needs no exact vmcnt across items, branches.
+template <bool NT = false>
 __device__ __forceinline__ void st_quad(const PassArgs& a, uint8_t* row, bool ok, const Thr& c, uint32_t L,
                                         uint32_t H) {
 #if RS16_ABLATE == 2
@@ -277,8 +310,8 @@ __device__ __forceinline__ void st_quad(const PassArgs& a, uint8_t* row, bool ok
 #else
     if (ok && c.active) {
         uint32_t* p = (uint32_t*)(row + c.offL);
-        p[0] = L;
-        p[8] = H;
+        st_dword<NT>(p, L);
+        st_dword<NT>(p + 8, H);
     }
 #endif
 }
@@ -1047,16 +1080,16 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         const uint32_t k = kidx<T, END_B>(c, m);
         const uint32_t r = row_rel<T>(cs, a, k);
         if constexpr (PT::STORE == ST_PLAIN) {
-            st_quad(a, a.out + (uint64_t)r * a.S_out, P != DEC_MID || (k >= a.need_lo && k < a.need_hi), cs, L[m], H[m]);
+            st_quad<ProgTraits<P>::ST_NT>(a, a.out + (uint64_t)r * a.S_out, P != DEC_MID || (k >= a.need_lo && k < a.need_hi), cs, L[m], H[m]);
         } else if constexpr (PT::STORE == ST_RECOVERY) {
-            st_quad(a, a.out + (uint64_t)r * a.S_out, r < a.out_rows, cs, L[m], H[m]);
+            st_quad<ProgTraits<P>::ST_NT>(a, a.out + (uint64_t)r * a.S_out, r < a.out_rows, cs, L[m], H[m]);
         } else {
             uint32_t tt[20];
             load_table_lds(tt, rvt + k * 5);
             uint32_t ol = 0, oh = 0;
             mul_xor(ol, oh, L[m], H[m], tt);
             const uint32_t i = r + a.row_base_out - (a.rest_seg_b ? a.chunk : 0);
-            st_quad(a, a.rest + (uint64_t)i * a.S_rest, lostf[k] != 0, cs, ol, oh);
+            st_quad<ProgTraits<P>::ST_NT>(a, a.rest + (uint64_t)i * a.S_rest, lostf[k] != 0, cs, ol, oh);
         }
     }
     stamp(a, 10);

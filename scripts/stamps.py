@@ -50,6 +50,7 @@ def main():
     buf = DeviceArray(eng, nwg * 16 * 8)
     err = RS16Error()
     out = {}
+    raw = {}
     for name in ["ENC_FIRST", "ENC_MID", "ENC_LAST", "DEC_HALF_FIRST", "DEC_HALF_MID", "DEC_HALF_LAST"]:
         buf.upload(np.zeros(nwg * 16, np.uint64))
         lib().rs16_engine_set_stamps(eng.h, buf.ptr, names[name], C.byref(err))
@@ -60,6 +61,7 @@ def main():
         st = st[st[:, 0] != 0]
         if len(st) == 0:
             continue
+        raw[name] = st
         rt0 = st[:, 14].min()
         start_us = (st[:, 14] - rt0) / 100.0
         end_us = (st[:, 15] - rt0) / 100.0
@@ -78,9 +80,28 @@ def main():
             "lifetime_median_us": round(float(np.median(end_us - start_us)), 2),
             "phase_median_us": phases,
         }
+        # by XCD (HW reg XCC_ID) and by start order within a CU (HW_ID cu/sh/se)
+        xcc = st[:, 13] & 15
+        by = {}
+        for x in np.unique(xcc):
+            sel = xcc == x
+            by[int(x)] = [round(float(np.median(end_us[sel])), 1), round(float(end_us[sel].max()), 1),
+                          round(float(np.median((end_us - start_us)[sel])), 1)]
+        out[name]["xcd_end_median_max_life"] = by
+        hw = st[:, 12]
+        cu = (xcc << 16) | (((hw >> 8) & 15) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 7) << 5))
+        rank = np.zeros(len(st), np.int64)
+        for c in np.unique(cu):
+            idx = np.nonzero(cu == c)[0]
+            rank[idx[np.argsort(start_us[idx], kind="stable")]] = np.arange(len(idx))
+        out[name]["cu_rank_life_median"] = {int(r): round(float(np.median((end_us - start_us)[rank == r])), 1)
+                                            for r in np.unique(rank)}
+        out[name]["cu_rank_end_median"] = {int(r): round(float(np.median(end_us[rank == r])), 1)
+                                           for r in np.unique(rank)}
         print(name, json.dumps(out[name]), flush=True)
     (ROOT / "gpurun_out").mkdir(exist_ok=True)
     (ROOT / "gpurun_out" / "stamps.json").write_text(json.dumps(out, indent=1))
+    np.savez_compressed(ROOT / "gpurun_out" / "stamps_raw.npz", **raw)
 
 
 if __name__ == "__main__":
