@@ -3,8 +3,14 @@ counter over dispatches (counters summed over XCD/SE instances per dispatch)."""
 import csv, sys, glob, collections, re
 def short(n):
     m = re.search(r"pass_kernel<(\d+), (\d+)>", n)
-    progs = ["GEN_FFT","GEN_IFFT","ENC_FIRST","ENC_MID","ENC_LAST","ENC_SINGLE","DEC_FIRST","DEC_MID","DEC_LAST","DEC_SINGLE"]
-    if m: return f"{progs[int(m.group(1))]}/T{m.group(2)}"
+    progs = ["GEN_FFT","GEN_IFFT","ENC_FIRST","ENC_MID","ENC_LAST","ENC_SINGLE","DEC_FIRST","DEC_MID","DEC_LAST",
+             "DEC_SINGLE","DEC_HALF_LAST","DEC_HALF_SINGLE"]
+    # the half-transform decode runs DEC_FIRST (T7) as DEC_HALF_FIRST and
+    # ENC_MID (T8) as DEC_HALF_MID: those rows average both uses
+    alias = {("ENC_MID", "8"): "ENC_MID+DEC_HALF_MID", ("DEC_FIRST", "7"): "DEC_HALF_FIRST"}
+    if m:
+        name = progs[int(m.group(1))]
+        return f"{alias.get((name, m.group(2)), name)}/T{m.group(2)}"
     return n.split("(")[0].replace("void rs16::","")[:28]
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
 cnt = collections.defaultdict(lambda: collections.defaultdict(set))
