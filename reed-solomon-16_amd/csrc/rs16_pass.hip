@@ -187,6 +187,7 @@ template <int T> __device__ __forceinline__ uint32_t row_rel(const Thr& c, const
 //   -DRS16_ABLATE=2  compile HBM loads/stores out (compute only)
 //   -DRS16_ABLATE=3  as 1, and no table staging
 //   -DRS16_ABLATE=4  as 1, and no LDS exchanges / formal derivative
+//   -DRS16_ABLATE=5  loads / stores kept, but to L2-resident scratch (no HBM)
 #ifndef RS16_ABLATE
 #define RS16_ABLATE 0
 #endif
@@ -285,6 +286,9 @@ __device__ __forceinline__ void ld_quad(const PassArgs& a, const uint8_t* row, b
     H = p[8];
 #else
     L = H = 0;
+#if RS16_ABLATE == 5
+    row = a.zero + (((uintptr_t)row >> 10) & 15) * 1024;  // L2-resident 16 KiB
+#endif
     if (ok && c.active) {
         const uint32_t* p = (const uint32_t*)(row + c.offL);
         L = ld_dword(p);
@@ -308,6 +312,9 @@ __device__ __forceinline__ void st_quad(const PassArgs& a, uint8_t* row, bool ok
     p[0] = L;
     p[8] = H;
 #else
+#if RS16_ABLATE == 5
+    row = a.sink + (((uintptr_t)row >> 10) & 255) * 1024;  // L2-resident 256 KiB
+#endif
     if (ok && c.active) {
         uint32_t* p = (uint32_t*)(row + c.offL);
         st_dword<NT>(p, L);

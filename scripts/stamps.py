@@ -11,6 +11,7 @@ direction done, 6 formal derivative, 7 layout-B FFT layers, 8 layout
 switch, 9 last layers, 10 stores issued, 11 stores done."""
 import ctypes as C
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -44,7 +45,8 @@ def main():
     for _ in range(3):
         step()
     eng.synchronize()
-    assert np.array_equal(d_rest.download(shape=(k, S)), original)
+    if not os.environ.get("RS16_NO_VERIFY"):
+        assert np.array_equal(d_rest.download(shape=(k, S)), original)
     names = {lib().rs16_prog_name(i).decode(): i for i in range(lib().rs16_prog_count())}
     nwg = 8192
     buf = DeviceArray(eng, nwg * 16 * 8)
@@ -100,7 +102,7 @@ def main():
                                            for r in np.unique(rank)}
         print(name, json.dumps(out[name]), flush=True)
     (ROOT / "gpurun_out").mkdir(exist_ok=True)
-    (ROOT / "gpurun_out" / "stamps.json").write_text(json.dumps(out, indent=1))
+    (ROOT / "gpurun_out" / os.environ.get("RS16_STAMPS_OUT", "stamps.json")).write_text(json.dumps(out, indent=1))
     np.savez_compressed(ROOT / "gpurun_out" / "stamps_raw.npz", **raw)
 
 
