@@ -86,6 +86,11 @@ struct PassArgs {
     // consumed downstream; FFT groups and stores outside it are skipped.
     // need_hi == 0: no pruning.
     uint32_t need_lo, need_hi;
+    // Set by launch_pass: every lane's byte offset within its wave's row
+    // (row-set offset x stride + quad offset) fits in 32 bits, and no wave's
+    // rows straddle the decoder's segment boundary, so HBM addresses are an
+    // SGPR row base + a 32-bit lane offset (else 64-bit lane offsets).
+    uint32_t voff32;
     // Decode zero tiles: zflags[t] = 1 when DEC_FIRST tile t holds no received
     // row (then it is all zero after the erasure multiply and is neither
     // computed nor stored).  Written with rbits by the eval_poly kernels from

@@ -181,6 +181,40 @@ template <int T, bool LB> __device__ __forceinline__ uint32_t kidx(const Thr& c,
 template <int T> __device__ __forceinline__ uint32_t row_rel(const Thr& c, const PassArgs& a, uint32_t k) {
     return c.b_low + (k << a.lo) + (c.b_high << (a.lo + T));
 }
+// row_rel(kidx(m)) split into a wave-uniform part (the row of the wave's
+// first row set, in SGPRs) and the lane's row-set offset (a VGPR that does
+// not depend on m): the HBM row addresses become one scalar multiply-add per
+// row plus a per-lane byte offset computed once (PassArgs::voff32).
+template <int T, bool LB> __device__ __forceinline__ uint32_t lane_rows(const Thr& c, const PassArgs& a) {
+    const uint32_t hs = c.s - c.w * Geo<T>::HWS;  // row set within the wave
+    return (LB ? hs : hs << Geo<T>::R) << a.lo;
+}
+// (the wave's row of row register 0, read into SGPRs once per item: a
+// readfirstlane inside the per-row branches would be repeated per row)
+template <int T, bool LB> struct WaveRows {
+    uint32_t base, lo;
+    __device__ __forceinline__ WaveRows(const Thr& c, const PassArgs& a) : lo(a.lo) {
+        const uint32_t sw = uni(c.w) * Geo<T>::HWS;
+        base = uni(c.b_low + (c.b_high << (a.lo + T)) + ((LB ? sw : sw << Geo<T>::R) << a.lo));
+    }
+    __device__ __forceinline__ uint32_t operator()(int m) const {
+        return base + ((LB ? (uint32_t)m << Geo<T>::SHB : (uint32_t)m) << lo);
+    }
+};
+// A wave-uniform row base address, pinned to SGPRs so that the compiler
+// adds the lane offset in the load / store itself (SGPR base + VGPR offset)
+// instead of folding the row product into a per-lane 64-bit multiply-add.
+typedef __attribute__((address_space(1))) uint8_t gbyte;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ gbyte* sgpr_ptr(const uint8_t* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = uni((uint32_t)v), hi = uni((uint32_t)(v >> 32));
+    return (gbyte*)(((uint64_t)hi << 32) | lo);
+}
+// r = ur + lr < lim for a uniform ur and a per-lane lr (one vector compare)
+__device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim) {
+    return ur < lim && lr < lim - ur;
+}
 
 // Diagnostic ablation builds (never the shipped library):
 //   -DRS16_ABLATE=1  compile the butterfly layers out (memory + staging only)
@@ -322,6 +356,60 @@ __device__ __forceinline__ void st_quad(const PassArgs& a, uint8_t* row, bool ok
     }
 #endif
 }
+
+// The same for a row address that already includes the lane's offset.
+__device__ __forceinline__ void ld_ptr(const PassArgs& a, const gbyte* p, bool ok, uint32_t& L, uint32_t& H) {
+#if RS16_ABLATE == 2
+    L = (uint32_t)(uintptr_t)p ^ (ok ? 1u : 0u);
+    H = L * 3u;
+    return;
+#endif
+#if RS16_ABLATE == 5
+    p = (const gbyte*)(a.zero + ((uintptr_t)p & 0x3FFCu));  // L2-resident 16 KiB
+#endif
+    (void)a;
+    L = H = 0;
+    if (ok) {
+        // (global address space from the SGPR base on: base + 32-bit lane
+        // offset selects the SGPR-base form of global_load)
+        const gu32* g = (const gu32*)p;
+        L = g[0];
+        H = g[8];
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void st_ptr(const PassArgs& a, gbyte* p, bool ok, uint32_t L, uint32_t H) {
+#if RS16_ABLATE == 2
+    if ((L ^ H) != 0x9e3779b9u) return;
+#endif
+#if RS16_ABLATE == 5
+    p = (gbyte*)(a.sink + ((uintptr_t)p & 0x3FFFCu));  // L2-resident 256 KiB
+#endif
+    (void)a;
+    if (ok) {
+        gu32* g = (gu32*)p;
+        if constexpr (NT) {
+            __builtin_nontemporal_store(L, g);
+            __builtin_nontemporal_store(H, g + 8);
+        } else {
+            g[0] = L;
+            g[8] = H;
+        }
+    }
+}
+// Per-lane byte offset of the lane's quad in the row lane_rows below the
+// wave's row: 32 bits (global_load/store with an SGPR base) when the launch
+// allows it (PassArgs::voff32), else 64 bits.
+template <bool V32> struct LaneOff {
+    uint32_t v;
+    __device__ __forceinline__ LaneOff(uint32_t lr, uint64_t S, uint32_t offL) : v(lr * (uint32_t)S + offL) {}
+    template <class B> __device__ __forceinline__ B* at(B* base) const { return base + v; }
+};
+template <> struct LaneOff<false> {
+    uint64_t v;
+    __device__ __forceinline__ LaneOff(uint32_t lr, uint64_t S, uint32_t offL) : v((uint64_t)lr * S + offL) {}
+    template <class B> __device__ __forceinline__ B* at(B* base) const { return base + v; }
+};
 
 __device__ __forceinline__ void load_table_lds(uint32_t (&t)[20], const uint4* p) {
 #pragma unroll
@@ -770,13 +858,83 @@ __device__ __forceinline__ void set_item(Thr& c, const PassArgs& a, uint32_t ite
     c.offL = (Qg >> 3) * 64 + (Qg & 7) * 4;
 }
 
+// The one-item build's row loads of an item: row address = SGPR base of the
+// wave's row (one scalar multiply-add per row) + the lane's offset.
+template <int P, int T, bool V32>
+__device__ __forceinline__ void load_rows(const PassArgs& a, const Thr& c, uint32_t tile, ItemRegs<P, T>& d) {
+    using PT = ProgTraits<P>;
+    using G = Geo<T>;
+    constexpr int NR = G::NR, R = G::R;
+    constexpr bool START_B = !PT::IFFT;
+    const uint32_t lr = lane_rows<T, START_B>(c, a);
+    const WaveRows<T, START_B> wr(c, a);
+    if constexpr (PT::LOAD == LD_PLAIN) {
+        const LaneOff<V32> lo(lr, a.S_in, c.offL);
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t ur = wr(m);
+            ld_ptr(a, lo.at(sgpr_ptr(a.in + (uint64_t)ur * a.S_in)), c.active & !((d.zrow >> m) & 1u), d.L[m], d.H[m]);
+        }
+    } else if constexpr (PT::LOAD == LD_GATHER_ENC) {
+        // HighRateEncoder::encode: work[0..k) = originals, rest zero (rate_high.rs:50-54)
+        const LaneOff<V32> lo(lr, a.S_seg, c.offL);
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t ur = wr(m);
+            ld_ptr(a, lo.at(sgpr_ptr(a.seg_a + (uint64_t)ur * a.S_seg)), c.active & row_below(ur, lr, a.a_count),
+                   d.L[m], d.H[m]);
+        }
+    } else if constexpr (PT::LOAD == LD_GATHER_DEC) {
+        // received rows (multiplied by their erasure logs in process_item), else
+        // zero.  Received bits of the wave's rows: rows [row0, row0 + 16 HWS)
+        // of the bitmap (row0 a multiple of 16, of 32 when HWS > 1), scalar loads.
+        static_assert(START_B == false && T <= 8, "gather runs in layout A");
+        const uint32_t row0 = row_rel<T>(c, a, (c.w * G::HWS) << R) + a.row_base_in;
+        const cu32p rb = (cu32p)a.rbits + (row0 >> 5);
+        const uint32_t sub = c.s - c.w * G::HWS;
+        uint32_t bits;
+        // (uni(): each word stays a scalar load; a select of two loads would
+        // be folded into one per-lane vector load)
+        if constexpr (G::HWS == 4) bits = ((sub >> 1) ? uni(rb[1]) : uni(rb[0])) >> ((sub & 1) * 16);
+        else if constexpr (G::HWS == 2) bits = uni(rb[0]) >> (sub * 16);
+        else bits = uni(rb[0]) >> (row0 & 31);
+        bits &= (1u << NR) - 1;
+        const LaneOff<V32> lo(lr, a.S_seg, c.offL);
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t ur = wr(m) + a.row_base_in;
+            const gbyte* p;
+            if constexpr (V32) {
+                // (voff32: the wave's rows never straddle the segment boundary)
+                p = lo.at(sgpr_ptr(ur >= a.chunk ? a.seg_b + (int64_t)((int64_t)ur - a.chunk) * (int64_t)a.S_seg
+                                                 : a.seg_a + (uint64_t)ur * a.S_seg));
+            } else {
+                const uint32_t r = ur + lr;
+                p = (const gbyte*)((r >= a.chunk ? a.seg_b + (uint64_t)(r - a.chunk) * a.S_seg
+                                                 : a.seg_a + (uint64_t)r * a.S_seg) +
+                                   c.offL);
+            }
+            ld_ptr(a, p, c.active & ((bits >> m) & 1u), d.L[m], d.H[m]);
+        }
+    } else {  // LD_DEC_LAST: u in registers, z for y = u + L(z)
+        d.ztile = a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u);
+        const LaneOff<V32> lo(lr, a.S_in, c.offL);
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t ur = wr(m);
+            ld_ptr(a, lo.at(sgpr_ptr(a.in + (uint64_t)ur * a.S_in)), c.active & !d.ztile, d.zl[m], d.zh[m]);
+            ld_ptr(a, lo.at(sgpr_ptr(a.in2 + (uint64_t)ur * a.S_in)), c.active, d.L[m], d.H[m]);
+        }
+    }
+}
+
 // Issue the HBM loads of one item (and read its decode flags).
 template <int P, int T>
 __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint32_t tile, ItemRegs<P, T>& d) {
     using PT = ProgTraits<P>;
     using G = Geo<T>;
     constexpr int NR = G::NR, R = G::R;
-    constexpr bool START_B = !PT::IFFT;
+    [[maybe_unused]] constexpr bool START_B = !PT::IFFT;
     d.zrow = d.zmask = 0;
     d.ztile = false;
     // ---------------- zero rows of DEC_MID ----------------
@@ -806,6 +964,11 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
                 if ((zf[4 * j] & zf[4 * j + 1] & zf[4 * j + 2] & zf[4 * j + 3]) == 0x01010101u) d.zmask |= 1u << j;
         }
     }
+#if !RS16_PIPE
+    if (a.voff32) load_rows<P, T, true>(a, c, tile, d);
+    else load_rows<P, T, false>(a, c, tile, d);
+}
+#else
     if constexpr (PT::LOAD == LD_PLAIN) {
 #pragma unroll
         for (int m = 0; m < NR; m++) {
@@ -851,6 +1014,7 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
         }
     }
 }
+#endif
 
 // Stage everything that depends on the tile key of the thread's current
 // item: twiddle tables of both directions, and for the decoder's first /
@@ -963,6 +1127,51 @@ __device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint
 
 // Compute and store one item whose rows are in d (every thread of the
 // workgroup calls it for the same item).
+// The one-item build's row stores of an item (the counterpart of load_rows).
+template <int P, int T, bool V32>
+__device__ __forceinline__ void store_rows(const PassArgs& a, const Thr& cs, const uint32_t (&L)[Geo<T>::NR],
+                                           const uint32_t (&H)[Geo<T>::NR], const uint4* rvt, const uint32_t* lostf) {
+    using PT = ProgTraits<P>;
+    constexpr int NR = Geo<T>::NR;
+    constexpr bool END_B = !PT::FFT && T > 4;
+    constexpr bool NT = PT::ST_NT;
+    const uint32_t lr = lane_rows<T, END_B>(cs, a);
+    const WaveRows<T, END_B> wr(cs, a);
+    if constexpr (PT::STORE == ST_PLAIN) {
+        const LaneOff<V32> lo(lr, a.S_out, cs.offL);
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t k = kidx<T, END_B>(cs, m);
+            const uint32_t ur = wr(m);
+            st_ptr<NT>(a, lo.at(sgpr_ptr(a.out + (uint64_t)ur * a.S_out)),
+                       cs.active & (P != DEC_MID || (k >= a.need_lo && k < a.need_hi)), L[m], H[m]);
+        }
+    } else if constexpr (PT::STORE == ST_RECOVERY) {
+        const LaneOff<V32> lo(lr, a.S_out, cs.offL);
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t ur = wr(m);
+            st_ptr<NT>(a, lo.at(sgpr_ptr(a.out + (uint64_t)ur * a.S_out)), cs.active & row_below(ur, lr, a.out_rows), L[m],
+                       H[m]);
+        }
+    } else {
+        // lost original row r -> restored-originals row r + row_base_out - (segment start)
+        const LaneOff<V32> lo(lr, a.S_rest, cs.offL);
+        const int64_t shift = (int64_t)a.row_base_out - (a.rest_seg_b ? (int64_t)a.chunk : 0);
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t k = kidx<T, END_B>(cs, m);
+            uint32_t tt[20];
+            load_table_lds(tt, rvt + k * 5);
+            uint32_t ol = 0, oh = 0;
+            mul_xor(ol, oh, L[m], H[m], tt);
+            const uint32_t ur = wr(m);
+            st_ptr<NT>(a, lo.at(sgpr_ptr(a.rest + ((int64_t)ur + shift) * (int64_t)a.S_rest)), cs.active & (lostf[k] != 0),
+                       ol, oh);
+        }
+    }
+}
+
 template <int P, int T>
 __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, uint32_t tile, uint32_t slab,
                                              ItemRegs<P, T>& d, uint8_t* smem) {
@@ -984,7 +1193,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     uint32_t(&H)[NR] = d.H;
     constexpr bool START_B = !PT::IFFT;
     // Final layout: after FFT -> A; after IFFT only -> B (T > 4); T <= 4: A == B.
-    constexpr bool END_B = !PT::FFT && T > 4;
+    [[maybe_unused]] constexpr bool END_B = !PT::FFT && T > 4;
 
     if constexpr (P == DEC_FIRST) {
         // A tile without received rows is zero after the erasure multiply
@@ -1080,8 +1289,14 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     // coordinates: otherwise the compiler keeps the load-time addresses of
     // the same rows live through all the butterflies (32 VGPRs).
     Thr cs = c;
+    cs.b_low = uni(cs.b_low);
+    cs.b_high = uni(cs.b_high);
     asm volatile("" : "+s"(cs.b_low), "+s"(cs.b_high));
     asm volatile("" : "+v"(cs.offL));
+#if !RS16_PIPE
+    if (a.voff32) store_rows<P, T, true>(a, cs, L, H, rvt, lostf);
+    else store_rows<P, T, false>(a, cs, L, H, rvt, lostf);
+#else
 #pragma unroll
     for (int m = 0; m < NR; m++) {
         const uint32_t k = kidx<T, END_B>(c, m);
@@ -1099,6 +1314,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             st_quad<ProgTraits<P>::ST_NT>(a, a.rest + (uint64_t)i * a.S_rest, lostf[k] != 0, cs, ol, oh);
         }
     }
+#endif
     stamp(a, 10);
 #if RS16_STAMPS
     __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
@@ -1240,6 +1456,14 @@ hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles
     a.per_wg = (uint32_t)((items + max_wg - 1) / max_wg);
     const uint32_t nwg = (uint32_t)((items + a.per_wg - 1) / a.per_wg);
     if (a.need_hi == 0) a.need_hi = 1u << T;  // no pruning
+    {
+        const uint64_t hws = kQuads[T] >= 64 ? 1 : 64 / kQuads[T];
+        const uint64_t smax = std::max(std::max(a.S_in, a.S_out), std::max(a.S_seg, a.S_rest));
+        const uint64_t span = (uint64_t)1 << (T + a.lo);  // rows of one tile's aligned block
+        const bool fits = (hws - 1) * ((uint64_t)16 << a.lo) * smax + 1024 < ((uint64_t)1 << 32);
+        const bool aligned = a.chunk % span == 0 && a.row_base_in % span == 0;
+        a.voff32 = fits && aligned ? 1u : 0u;
+    }
     const size_t lds = (size_t)kSmem[prog][T];
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)kPass[prog][T], hipFuncAttributeMaxDynamicSharedMemorySize,
