@@ -1462,7 +1462,12 @@ hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles
         const uint64_t span = (uint64_t)1 << (T + a.lo);  // rows of one tile's aligned block
         const bool fits = (hws - 1) * ((uint64_t)16 << a.lo) * smax + 1024 < ((uint64_t)1 << 32);
         const bool aligned = a.chunk % span == 0 && a.row_base_in % span == 0;
-        a.voff32 = fits && aligned ? 1u : 0u;
+        // RS16_FORCE_VOFF64=1 (tests): always the 64-bit lane offsets
+        static const bool force64 = [] {
+            const char* e = std::getenv("RS16_FORCE_VOFF64");
+            return e && e[0] == '1';
+        }();
+        a.voff32 = fits && aligned && !force64 ? 1u : 0u;
     }
     const size_t lds = (size_t)kSmem[prog][T];
     if (lds > 65536) {
