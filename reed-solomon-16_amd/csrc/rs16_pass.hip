@@ -1325,6 +1325,9 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
 // The persistent pass: workgroup b processes items [b * per_wg, ...) of the
 // launch, loading item i + 1 while it computes item i.
 template <int P, int T>
+#ifndef RS16_LDPRIO
+#define RS16_LDPRIO 1
+#endif
 #ifndef RS16_MINW
 #define RS16_MINW (RS16_PIPE ? 2 : 4)
 #endif
@@ -1355,6 +1358,18 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     // tables are requested first, the tile's rows right behind them, so the
     // staging latency hides under the row loads.
     stamp(a, 0);
+#if RS16_LDPRIO
+    // Load-issue order: the workgroup in slot 0 of its CU (HW_ID.tg_id) issues
+    // its rows first, slot 1 next, ...  Same-box A/B: kernel times equal,
+    // step time -2 % (643-645 -> 654-659 GiB/s, 3 pairs).  The progress-based
+    // schedule (prio<P, at>) takes over once the tables are staged.
+    if constexpr (T >= 7) {
+        const uint32_t slot = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 16) & 15u;
+        if (slot == 0) __builtin_amdgcn_s_setprio(3);
+        else if (slot == 1) __builtin_amdgcn_s_setprio(2);
+        else if (slot == 2) __builtin_amdgcn_s_setprio(1);
+    }
+#endif
     TileStage<P, T> st;
     st.issue(a, c);  // twiddle tables first: they do not queue behind the tile
     ItemRegs<P, T> cur;
@@ -1469,7 +1484,16 @@ hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles
         }();
         a.voff32 = fits && aligned && !force64 ? 1u : 0u;
     }
-    const size_t lds = (size_t)kSmem[prog][T];
+    size_t lds = (size_t)kSmem[prog][T];
+    {
+        // RS16_LDS_PAD_T7=<bytes> (experiment): extra LDS per workgroup of the
+        // T = 7 passes, to cap the resident workgroups per CU
+        static const size_t pad = [] {
+            const char* e = std::getenv("RS16_LDS_PAD_T7");
+            return e ? (size_t)std::atoll(e) : (size_t)0;
+        }();
+        if (T == 7) lds += pad;
+    }
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)kPass[prog][T], hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);
