@@ -397,6 +397,20 @@ __device__ __forceinline__ void st_ptr(const PassArgs& a, gbyte* p, bool ok, uin
         }
     }
 }
+// Branch-free: a row that is not read is read from the zero page instead
+// (PassArgs::zero), so the item's loads are a fixed sequence and the
+// compiler's vmcnt waits (for the staged tables and erasure logs, issued
+// before the rows) count exactly instead of waiting for every row.
+__device__ __forceinline__ void ld_sel(const PassArgs& a, const gbyte* p, bool ok, uint32_t offL, uint32_t& L,
+                                       uint32_t& H) {
+#if RS16_ABLATE == 2 || RS16_ABLATE == 5
+    ld_ptr(a, p, ok, L, H);
+#else
+    const gu32* g = (const gu32*)(ok ? p : (const gbyte*)a.zero + offL);
+    L = g[0];
+    H = g[8];
+#endif
+}
 // Per-lane byte offset of the lane's quad in the row lane_rows below the
 // wave's row: 32 bits (global_load/store with an SGPR base) when the launch
 // allows it (PassArgs::voff32), else 64 bits.
@@ -873,7 +887,7 @@ __device__ __forceinline__ void load_rows(const PassArgs& a, const Thr& c, uint3
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t ur = wr(m);
-            ld_ptr(a, lo.at(sgpr_ptr(a.in + (uint64_t)ur * a.S_in)), c.active & !((d.zrow >> m) & 1u), d.L[m], d.H[m]);
+            ld_sel(a, lo.at(sgpr_ptr(a.in + (uint64_t)ur * a.S_in)), c.active & !((d.zrow >> m) & 1u), c.offL, d.L[m], d.H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_ENC) {
         // HighRateEncoder::encode: work[0..k) = originals, rest zero (rate_high.rs:50-54)
@@ -881,8 +895,8 @@ __device__ __forceinline__ void load_rows(const PassArgs& a, const Thr& c, uint3
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t ur = wr(m);
-            ld_ptr(a, lo.at(sgpr_ptr(a.seg_a + (uint64_t)ur * a.S_seg)), c.active & row_below(ur, lr, a.a_count),
-                   d.L[m], d.H[m]);
+            ld_sel(a, lo.at(sgpr_ptr(a.seg_a + (uint64_t)ur * a.S_seg)), c.active & row_below(ur, lr, a.a_count),
+                   c.offL, d.L[m], d.H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_DEC) {
         // received rows (multiplied by their erasure logs in process_item), else
@@ -914,7 +928,7 @@ __device__ __forceinline__ void load_rows(const PassArgs& a, const Thr& c, uint3
                                                  : a.seg_a + (uint64_t)r * a.S_seg) +
                                    c.offL);
             }
-            ld_ptr(a, p, c.active & ((bits >> m) & 1u), d.L[m], d.H[m]);
+            ld_sel(a, p, c.active & ((bits >> m) & 1u), c.offL, d.L[m], d.H[m]);
         }
     } else {  // LD_DEC_LAST: u in registers, z for y = u + L(z)
         d.ztile = a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u);
@@ -922,8 +936,8 @@ __device__ __forceinline__ void load_rows(const PassArgs& a, const Thr& c, uint3
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const uint32_t ur = wr(m);
-            ld_ptr(a, lo.at(sgpr_ptr(a.in + (uint64_t)ur * a.S_in)), c.active & !d.ztile, d.zl[m], d.zh[m]);
-            ld_ptr(a, lo.at(sgpr_ptr(a.in2 + (uint64_t)ur * a.S_in)), c.active, d.L[m], d.H[m]);
+            ld_sel(a, lo.at(sgpr_ptr(a.in + (uint64_t)ur * a.S_in)), c.active & !d.ztile, c.offL, d.zl[m], d.zh[m]);
+            ld_sel(a, lo.at(sgpr_ptr(a.in2 + (uint64_t)ur * a.S_in)), c.active, c.offL, d.L[m], d.H[m]);
         }
     }
 }
