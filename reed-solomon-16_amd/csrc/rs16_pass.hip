@@ -1082,6 +1082,12 @@ template <int P, int T> struct TileStage {
     Stager<T, N2> s2;
 
     uint32_t ev[4];  // wave 0: the tile's 256-row block of eval_poly's work (ework)
+    // decoder gather: the received-bitmap words of this thread's erasure-table
+    // rows, loaded before the tile's rows so that the table loads that depend
+    // on them issue back to back (a per-row flag load after the rows would
+    // wait for all of them, once per table)
+    static constexpr int PER_E = ((1 << T) * 5 + G::THREADS - 1) / G::THREADS;
+    uint32_t rw[PT::LOAD == LD_GATHER_DEC ? PER_E : 1];
 
     // the 256-row block holding the tile's decode rows (contiguous tiles of
     // 2^T <= 256 rows at a multiple of 2^T lie in one block)
@@ -1096,6 +1102,14 @@ template <int P, int T> struct TileStage {
                 const uint32_t* src = a.ework + (elog_row0(a, c) & ~255u) + c.lane;
 #pragma unroll
                 for (int j = 0; j < 4; j++) ev[j] = src[64 * j];
+            }
+        }
+        if constexpr (PT::LOAD == LD_GATHER_DEC) {
+#pragma unroll
+            for (int i = 0; i < PER_E; i++) {
+                const uint32_t idx = threadIdx.x + (uint32_t)i * G::THREADS;
+                const uint32_t k = min(idx / 5, (1u << T) - 1);
+                rw[i] = a.rbits[(row_rel<T>(c, a, k) + a.row_base_in) >> 5];
             }
         }
         s1.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
@@ -1117,8 +1131,26 @@ template <int P, int T> struct TileStage {
             }
         }
         if constexpr (PT::LOAD == LD_GATHER_DEC) {
+            // "MULTIPLY SHARDS" tables (GatherEntry, with the received bit from rw)
+            static_assert(PER_E == Stager<T, (1 << T)>::PER, "one table chunk per (thread, i)");
             Stager<T, (1 << T)> se;
-            se.issue(a.mul_tab, GatherEntry<T>{a, c, el});
+            const u32x4* tab = (const u32x4*)a.mul_tab;
+            // (two uniform paths: with the logs in LDS every table load issues
+            // back to back; only the HBM-logs path waits per row)
+            auto gather = [&](auto log_of) {
+#pragma unroll
+                for (int i = 0; i < PER_E; i++) {
+                    const uint32_t idx = threadIdx.x + (uint32_t)i * G::THREADS;
+                    const uint32_t k = min(idx / 5, (1u << T) - 1);
+                    const uint32_t r = row_rel<T>(c, a, k) + a.row_base_in;
+                    const bool rcv = (rw[i] >> (r & 31)) & 1u;
+                    const uint32_t e = rcv ? log_of(k, r) : ZERO_ENTRY;
+                    if (RS16_ABLATE != 3 && idx < (1u << T) * 5)
+                        se.v[i] = tab[(size_t)e * (TAB_DWORDS / 4) + idx % 5];
+                }
+            };
+            if (el) gather([&](uint32_t k, uint32_t) { return el[k]; });
+            else gather([&](uint32_t, uint32_t r) { return a.elog[r]; });
             se.commit((uint4*)(smem + SM::ERT_OFF));
         }
         if constexpr (PT::STORE == ST_RESTORE && !LateReveal<P, T>::value) {
