@@ -574,9 +574,29 @@ __device__ __forceinline__ void fwht256_wave(uint32_t (&v)[4]) {
 
 // Layers for k-bits [KB0, KB1) held in registers of layout LB, as a
 // compile-time sequence of twiddle groups (step s, index gi).
+// No per-group action (GroupLoop's default).
+struct NoFin {
+    template <class X> __device__ __forceinline__ void operator()(const X&, const X&, int) const {}
+};
+
+// Breadth-first (layer by layer), except the last FFT block in layout A of
+// all 4 register bits: there the groups run depth-first in pre-order (a
+// group, then its two halves), so rows m, m + 1 are final right after their
+// layer-0 group and can be stored there (EarlyStore).
+#ifndef RS16_EARLY_ST
+#define RS16_EARLY_ST 1
+#endif
 template <int T, bool LB, int KB0, int KB1, bool FFT> struct LayerSeq {
     static constexpr int SH = LB ? Geo<T>::SHB : 0;
     static constexpr int NR = Geo<T>::NR;
+    static constexpr bool DF = RS16_EARLY_ST && FFT && !LB && KB0 == 0 && KB1 == 4 && NR == 16;
+    // pre-order of the radix-16 group tree, (kb, gi) packed as kb * 16 + gi
+    static constexpr int df_at(int g) {
+        constexpr int ord[15] = {3 * 16 + 0, 2 * 16 + 0, 1 * 16 + 0, 0 * 16 + 0, 0 * 16 + 1, 1 * 16 + 1, 0 * 16 + 2,
+                                 0 * 16 + 3, 2 * 16 + 1, 1 * 16 + 2, 0 * 16 + 4, 0 * 16 + 5, 1 * 16 + 3, 0 * 16 + 6,
+                                 0 * 16 + 7};
+        return ord[g];
+    }
     static constexpr int kb_of(int s) { return FFT ? KB1 - 1 - s : KB0 + s; }
     static constexpr int groups_of(int s) { return NR >> (kb_of(s) - SH + 1); }
     static constexpr int total() {
@@ -585,11 +605,13 @@ template <int T, bool LB, int KB0, int KB1, bool FFT> struct LayerSeq {
         return n;
     }
     static constexpr int step_of(int g) {
+        if (DF) return KB1 - 1 - df_at(g) / 16;
         int s = 0;
         while (g >= groups_of(s)) g -= groups_of(s), s++;
         return s;
     }
     static constexpr int index_of(int g) {
+        if (DF) return df_at(g) % 16;
         int s = 0;
         while (g >= groups_of(s)) g -= groups_of(s), s++;
         return g;
@@ -635,10 +657,11 @@ template <int NR> __device__ __forceinline__ void pin_rows(uint32_t (&L)[NR], ui
 //   PR_ZERO IFFT: a group whose rows are all zero on input stays zero and is
 //           skipped.  zmask bit j = tile rows [16j, 16j+16) are all zero.
 enum { PR_NONE = 0, PR_OUT, PR_ZERO };
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, int G> struct GroupLoop {
+template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, int G, class FIN = NoFin>
+struct GroupLoop {
     static __device__ __forceinline__ void run(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                                const PassArgs& a, const uint4* tab1, const uint4* tab2,
-                                               const uint32_t (&cur)[20], uint32_t zmask) {
+                                               const uint32_t (&cur)[20], uint32_t zmask, const FIN& fin = FIN()) {
         using S = LayerSeq<T, LB, KB0, KB1, FFT>;
         constexpr int s = S::step_of(G), gi = S::index_of(G);
         constexpr int kb = S::kb_of(s);
@@ -676,20 +699,21 @@ template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, i
         pin_rows<Geo<T>::NR>(L, H);
 #endif
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (S::DF && kb == 0) fin(L, H, gi << 1);  // rows 2 gi, 2 gi + 1 are final
         if constexpr (more)
-            GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, G + 1>::run(L, H, c, a, tab1, tab2, nxt, zmask);
+            GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, G + 1, FIN>::run(L, H, c, a, tab1, tab2, nxt, zmask, fin);
     }
 };
 
 // Apply the layers for k-bits [KB0, KB1) held in registers of layout LB.
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE = PR_NONE>
+template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE = PR_NONE, class FIN = NoFin>
 __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                        const PassArgs& a, const uint4* tab1, const uint4* tab2,
-                                       uint32_t zmask = 0) {
-    if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2)) {
+                                       uint32_t zmask = 0, const FIN& fin = FIN()) {
+    if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6)) {
         uint32_t t0[20];
         load_table_lds(t0, group_table<T, LB, KB0, KB1, FFT, 0, IN_TAB2>(c, tab1, tab2));
-        GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0>::run(L, H, c, a, tab1, tab2, t0, zmask);
+        GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0, FIN>::run(L, H, c, a, tab1, tab2, t0, zmask, fin);
     }
 }
 
@@ -1173,50 +1197,65 @@ __device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint
 
 // Compute and store one item whose rows are in d (every thread of the
 // workgroup calls it for the same item).
-// The one-item build's row stores of an item (the counterpart of load_rows).
+// The one-item build's store of row register m of an item (the counterpart
+// of load_rows): recovery / work rows as they are, lost originals revealed
+// (x (65535 - e), rate_high.rs:236-242) into the caller's original array.
 template <int P, int T, bool V32>
-__device__ __forceinline__ void store_rows(const PassArgs& a, const Thr& cs, const uint32_t (&L)[Geo<T>::NR],
-                                           const uint32_t (&H)[Geo<T>::NR], const uint4* rvt, const uint32_t* lostf) {
+__device__ __forceinline__ void store_row(const PassArgs& a, const Thr& cs, uint32_t L, uint32_t H, int m,
+                                          const uint4* rvt, const uint32_t* lostf) {
     using PT = ProgTraits<P>;
-    constexpr int NR = Geo<T>::NR;
     constexpr bool END_B = !PT::FFT && T > 4;
     constexpr bool NT = PT::ST_NT;
     const uint32_t lr = lane_rows<T, END_B>(cs, a);
     const WaveRows<T, END_B> wr(cs, a);
+    const uint32_t ur = wr(m);
     if constexpr (PT::STORE == ST_PLAIN) {
         const LaneOff<V32> lo(lr, a.S_out, cs.offL);
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const uint32_t k = kidx<T, END_B>(cs, m);
-            const uint32_t ur = wr(m);
-            st_ptr<NT>(a, lo.at(sgpr_ptr(a.out + (uint64_t)ur * a.S_out)),
-                       cs.active & (P != DEC_MID || (k >= a.need_lo && k < a.need_hi)), L[m], H[m]);
-        }
+        const uint32_t k = kidx<T, END_B>(cs, m);
+        st_ptr<NT>(a, lo.at(sgpr_ptr(a.out + (uint64_t)ur * a.S_out)),
+                   cs.active & (P != DEC_MID || (k >= a.need_lo && k < a.need_hi)), L, H);
     } else if constexpr (PT::STORE == ST_RECOVERY) {
         const LaneOff<V32> lo(lr, a.S_out, cs.offL);
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const uint32_t ur = wr(m);
-            st_ptr<NT>(a, lo.at(sgpr_ptr(a.out + (uint64_t)ur * a.S_out)), cs.active & row_below(ur, lr, a.out_rows), L[m],
-                       H[m]);
-        }
+        st_ptr<NT>(a, lo.at(sgpr_ptr(a.out + (uint64_t)ur * a.S_out)), cs.active & row_below(ur, lr, a.out_rows), L, H);
     } else {
         // lost original row r -> restored-originals row r + row_base_out - (segment start)
         const LaneOff<V32> lo(lr, a.S_rest, cs.offL);
         const int64_t shift = (int64_t)a.row_base_out - (a.rest_seg_b ? (int64_t)a.chunk : 0);
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const uint32_t k = kidx<T, END_B>(cs, m);
-            uint32_t tt[20];
-            load_table_lds(tt, rvt + k * 5);
-            uint32_t ol = 0, oh = 0;
-            mul_xor(ol, oh, L[m], H[m], tt);
-            const uint32_t ur = wr(m);
-            st_ptr<NT>(a, lo.at(sgpr_ptr(a.rest + ((int64_t)ur + shift) * (int64_t)a.S_rest)), cs.active & (lostf[k] != 0),
-                       ol, oh);
-        }
+        const uint32_t k = kidx<T, END_B>(cs, m);
+        uint32_t tt[20];
+        load_table_lds(tt, rvt + k * 5);
+        uint32_t ol = 0, oh = 0;
+        mul_xor(ol, oh, L, H, tt);
+        st_ptr<NT>(a, lo.at(sgpr_ptr(a.rest + ((int64_t)ur + shift) * (int64_t)a.S_rest)), cs.active & (lostf[k] != 0),
+                   ol, oh);
     }
 }
+template <int P, int T, bool V32>
+__device__ __forceinline__ void store_rows(const PassArgs& a, const Thr& cs, const uint32_t (&L)[Geo<T>::NR],
+                                           const uint32_t (&H)[Geo<T>::NR], const uint4* rvt, const uint32_t* lostf) {
+#pragma unroll
+    for (int m = 0; m < Geo<T>::NR; m++) store_row<P, T, V32>(a, cs, L[m], H[m], m, rvt, lostf);
+}
+// Early stores: the last FFT block in layout A runs depth-first (LayerSeq),
+// so rows m, m + 1 are final as soon as their layer-0 group is done; this
+// functor stores them there, spreading the item's stores over the block
+// instead of a burst after it.
+template <int P, int T> struct EarlyStore {
+    const PassArgs& a;
+    const Thr& cs;
+    const uint4* rvt;
+    const uint32_t* lostf;
+    __device__ __forceinline__ void operator()(const uint32_t (&L)[Geo<T>::NR], const uint32_t (&H)[Geo<T>::NR],
+                                               int m) const {
+        if (a.voff32) {
+            store_row<P, T, true>(a, cs, L[m], H[m], m, rvt, lostf);
+            store_row<P, T, true>(a, cs, L[m + 1], H[m + 1], m + 1, rvt, lostf);
+        } else {
+            store_row<P, T, false>(a, cs, L[m], H[m], m, rvt, lostf);
+            store_row<P, T, false>(a, cs, L[m + 1], H[m + 1], m + 1, rvt, lostf);
+        }
+    }
+};
 
 template <int P, int T>
 __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, uint32_t tile, uint32_t slab,
@@ -1229,6 +1268,10 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     constexpr int NQR = Rnd<P, T>::NQR;
     constexpr bool TWO = SM::TWO;
     constexpr bool ZERO_SKIP = P == DEC_MID && T > 4;  // DEC_MID runs with T >= 5 only
+    // stores inside the last FFT block (one-item build, 16 rows per lane, not
+    // the output-pruned DEC_MID; the reveal stores measured slower inside it)
+    constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && !RS16_PIPE && P != DEC_MID && PT::STORE != ST_RESTORE &&
+                           (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6) && PT::FFT && T > 4;
     uint2* lds = (uint2*)smem;
     const uint4* tab1 = (const uint4*)(smem + SM::TAB1_OFF);
     const uint4* tab2 = (const uint4*)(smem + SM::TAB2_OFF);
@@ -1320,8 +1363,19 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         bool need = true;
         if constexpr (P == DEC_MID) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
         // second direction's layout-A tables: restaged into tab1 (T > 4), else in tab2
-        if (need) layers<T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2);
+        if constexpr (EARLY) {
+            Thr cs = c;
+            asm volatile("" : "+v"(cs.offL));
+            layers<T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2, 0,
+                                                                   EarlyStore<P, T>{a, cs, rvt, lostf});
+        } else if (need) {
+            layers<T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2);
+        }
         stamp(a, 9);
+    }
+    if constexpr (EARLY) {
+        stamp(a, 10);
+        return;
     }
 
     prio<P, 5>();
