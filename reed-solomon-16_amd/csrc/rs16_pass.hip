@@ -406,7 +406,8 @@ __device__ __forceinline__ void ld_sel(const PassArgs& a, const gbyte* p, bool o
 #if RS16_ABLATE == 2 || RS16_ABLATE == 5
     ld_ptr(a, p, ok, L, H);
 #else
-    const gu32* g = (const gu32*)(ok ? p : (const gbyte*)a.zero + offL);
+    // (offL & 0x7FFF: the zero page is RS16_ZERO_BYTES = 64 KiB, rows can be wider)
+    const gu32* g = (const gu32*)(ok ? p : (const gbyte*)a.zero + (offL & 0x7FFFu));
     L = g[0];
     H = g[8];
 #endif

@@ -100,9 +100,12 @@ def test_decode_nothing_to_do_and_not_enough(eng):
                                  recovery_received_count=1)
 
 
-@pytest.mark.parametrize("k,m,sb", [(32768, 32768, 64), (1000, 1000, 64 * 3), (300, 300, 64 * 9)])
+@pytest.mark.parametrize("k,m,sb", [(32768, 32768, 64), (1000, 1000, 64 * 3), (300, 300, 64 * 9),
+                                    (100, 100, 65536 + 192), (300, 600, 65536 + 192)])
 def test_odd_shard_widths(eng, k, m, sb):
-    # shard widths that are not a multiple of the 512-byte tile slab
+    # shard widths that are not a multiple of the 512-byte tile slab; rows
+    # wider than the 64 KiB zero page (the lanes past the last partial slab
+    # read from it at their in-row offset, masked into the page)
     original = generate_original(k, sb, 5)
     recovery = dev_encode(eng, original, m)
     assert np.array_equal(recovery, O.encode(k, m, original))
