@@ -28,3 +28,17 @@ for L1 in (327, 32768):
     eng.synchronize()
     print(L1, "per-call (launch, total) us:", [(round(p * 1e6), round(q * 1e6)) for p, q in per],
           "loop us/call:", round((time.perf_counter() - t) / 20 * 1e6), flush=True)
+
+# per-pass hipEvent times of the 1 %-loss (general) decode
+of = np.ones(k, np.uint8); of[k - 327:] = 0
+rf = np.zeros(m, np.uint8); rf[:327] = 1
+o1 = orig.copy(); o1[k - 327:] = 0
+a, b, x = DeviceArray.from_numpy(eng, of), DeviceArray.from_numpy(eng, rf), DeviceArray.from_numpy(eng, o1)
+eng.set_profiling(True)
+eng.profile_reset()
+for _ in range(10):
+    rs16.decode_device(k, m, S, x.ptr, a.ptr, d_r.ptr, b.ptr, k - 327, 327, engine=eng)
+eng.synchronize()
+prof = eng.profile()
+eng.set_profiling(False)
+print("1 % decode per pass (us):", {n: round(ms * 1e3 / max(c, 1), 2) for n, (ms, c) in prof.items() if c})
