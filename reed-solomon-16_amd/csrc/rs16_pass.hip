@@ -1376,6 +1376,10 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     }
     if constexpr (EARLY) {
         stamp(a, 10);
+#if RS16_STAMPS
+        __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
+        stamp(a, 11);
+#endif
         return;
     }
 
