@@ -299,6 +299,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.zflags = L > 8 ? (uint8_t*)ws_zflag.p : nullptr;
     es.n = g.n;
     es.zlo = (uint32_t)(L / 2);
+    es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
     // The decode passes that read erasure logs finish eval_poly's last
@@ -306,11 +307,11 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // (one kernel less) -- except the one-pass half-transform decode, whose
     // gather and reveal rows lie in different blocks.
     const bool small = g.high && g.n <= 2048 && !eval_full_forced();
-    elog_fused = !small && !(half_decode(g) && ilog2(g.n) - 1 <= 8);
+    elog_fused = !(half_decode(g) && ilog2(g.n) - 1 <= 8);
     if (small) {
         // erasures are zero from row n on: only n/256 live blocks (rs16_misc.hip)
         RS16_HIP(launch_eval_poly_small(es, (uint32_t)g.n, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh,
-                                        s));
+                                        s, !elog_fused));
     } else {
         RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s,
                                              !elog_fused));

@@ -140,12 +140,13 @@ struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.r
     uint32_t* rbits;
     uint8_t* zflags;
     uint32_t n, zlo;
+    uint64_t* stamps;          // RS16_STAMPS builds: eval timeline (rs16_engine_set_stamps)
 };
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo);
 // high-rate decodes with n <= 2048 rows (tail_fill == 0): 2 kernels, rows [0, n) of out_elog
 hipError_t launch_eval_poly_small(const ErasureSpec& e, uint32_t n, uint32_t* work, uint32_t* out_elog,
-                                  const uint16_t* log_walsh, hipStream_t s);
+                                  const uint16_t* log_walsh, hipStream_t s, bool last_lo);
 hipError_t launch_eval_poly_u16(uint16_t* data, uint32_t* work, const uint16_t* log_walsh, hipStream_t s);
 hipError_t launch_fwht_u16(uint16_t* data, uint32_t* work, hipStream_t s);
 

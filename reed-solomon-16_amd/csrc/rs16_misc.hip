@@ -110,31 +110,26 @@ __device__ __forceinline__ bool received_at(const ErasureSpec& e, uint32_t i) {
     if (i >= e.chunk && i - e.chunk < e.b_count) return e.flags_b ? ((cu8p)e.flags_b)[i - e.chunk] != 0 : true;
     return false;
 }
-// Received-row bitmap and zero-tile flags of rows [base, base + 256) (a
-// 256-thread block): rbits by wave ballots, zflags per tile of 2^zlo rows.
-__device__ __forceinline__ void decode_flags_block(const ErasureSpec& e, uint32_t base) {
-    __shared__ uint32_t words[8];
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const bool rcv = base + t < e.n && received_at(e, base + t);
-    const uint64_t b = __ballot(rcv);
-    if (lane == 0) {
-        words[2 * w] = (uint32_t)b;
-        words[2 * w + 1] = (uint32_t)(b >> 32);
-        if (e.rbits && base + 64 * w < e.n) {
-            e.rbits[(base >> 5) + 2 * w] = (uint32_t)b;
-            e.rbits[(base >> 5) + 2 * w + 1] = (uint32_t)(b >> 32);
+// Received-row bitmap and zero-tile flags of rows [base, base + 256) by one
+// wave, from the ballots rmask[j] of rows base + 64 j + lane: rbits words,
+// zflags per tile of 2^zlo rows.
+__device__ __forceinline__ void block_flags_wave(const ErasureSpec& e, uint32_t base, const uint64_t (&rmask)[4]) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (base >= e.n) return;
+    if (e.rbits && lane < 8 && base + 32u * lane < e.n)
+        e.rbits[(base >> 5) + lane] = (uint32_t)(rmask[lane >> 1] >> (32 * (lane & 1)));
+    if (e.zflags) {
+        const uint32_t ts = 1u << e.zlo, ntile = e.n >> e.zlo;
+        // tile t of this block: rows [t ts, (t + 1) ts), t < 256 / ts
+        for (uint32_t t = lane; t < 256u / ts; t += 64) {
+            bool any = false;
+            for (uint32_t r = t * ts; r < (t + 1) * ts; r += 64) {
+                const uint32_t w = r >> 6, sh = r & 63, len = ts < 64 ? ts : 64;
+                const uint64_t m = len == 64 ? ~0ull : ((1ull << len) - 1) << sh;
+                any |= (rmask[w] & m) != 0;
+            }
+            if ((base >> e.zlo) + t < ntile) e.zflags[(base >> e.zlo) + t] = any ? 0 : 1;
         }
-    }
-    if (!e.zflags) return;
-    __syncthreads();
-    const uint32_t ts = 1u << e.zlo, ntile = e.n >> e.zlo;
-    if (t < 256u / ts && ((base >> e.zlo) + t) < ntile) {
-        bool any = false;
-        for (uint32_t r = t * ts; r < (t + 1) * ts; r += 32) {
-            const uint32_t m = ts >= 32 ? 0xFFFFFFFFu : ((1u << ts) - 1) << (r & 31);
-            any |= (words[r >> 5] & m) != 0;
-        }
-        e.zflags[(base >> e.zlo) + t] = any ? 0 : 1;
     }
 }
 
@@ -208,23 +203,7 @@ __global__ void __launch_bounds__(64) fwht_lo_flags_kernel(ErasureSpec e, uint32
         v[j] = erasure_at(e, i);
         rmask[j] = __ballot(i < e.n && received_at(e, i));
     }
-    if (base < e.n) {
-        if (e.rbits && lane < 8 && base + 32u * lane < e.n)
-            e.rbits[(base >> 5) + lane] = (uint32_t)(rmask[lane >> 1] >> (32 * (lane & 1)));
-        if (e.zflags) {
-            const uint32_t ts = 1u << e.zlo, ntile = e.n >> e.zlo;
-            // tile t of this block: rows [t ts, (t + 1) ts), t < 256 / ts
-            for (uint32_t t = lane; t < 256u / ts; t += 64) {
-                bool any = false;
-                for (uint32_t r = t * ts; r < (t + 1) * ts; r += 64) {
-                    const uint32_t w = r >> 6, sh = r & 63, len = ts < 64 ? ts : 64;
-                    const uint64_t m = len == 64 ? ~0ull : ((1ull << len) - 1) << sh;
-                    any |= (rmask[w] & m) != 0;
-                }
-                if ((base >> e.zlo) + t < ntile) e.zflags[(base >> e.zlo) + t] = any ? 0 : 1;
-            }
-        }
-    }
+    block_flags_wave(e, base, rmask);
     fwht256_wave(v);
 #pragma unroll
     for (int j = 0; j < 4; j++) out32[base + lane + 64u * j] = v[j];
@@ -266,63 +245,136 @@ hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uin
 // the erasure vector is zero from row n on (rate_high.rs:183-197, the
 // truncation of the first fwht), so with H = H_lo H_hi only the NB = n/256
 // blocks of row bits 8-15 below n carry input, and only rows < n of the
-// output are consumed.  One workgroup per low index j (row bits 0-7):
-//   x[h']  = sum_i (-1)^|j&i| e[256h' + i]          (H_lo of the NB live blocks)
-//   w[h]   = LW[256h + j] * sum_h' (-1)^|h&h'| x[h'] (H_hi, x LogWalsh)
-//   z[h''] = sum_h (-1)^|h''&h| w[h],   h'' < NB     (H_hi, live outputs only)
-// as integer sums (|sum| < 2^24) reduced mod 65535 once; the last H_lo over the
-// NB output blocks is fwht_lo_kernel.  Same residues as the 3-kernel path.
-template <int NB> __device__ __forceinline__ void block_sum(int (&v)[NB], int (*sh)[4]) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
-        if (lane == 0) sh[k][w] = v[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NB; k++) v[k] = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
-    __syncthreads();
+// output are consumed.  One 256-thread workgroup per low index j (row bits
+// 0-7), thread t = row t of every block and h = t of the middle vector:
+//   x[h']  = sum_t (-1)^|j&t| e[256h' + t]            (H_lo of the NB live blocks)
+//   w[h]   = LW[256h + j] * sum_h' (-1)^|h&h'| x[h']   (H_hi, x LogWalsh)
+//   z[h''] = sum_h (-1)^|h''&h| w[h],   h'' < NB       (H_hi, live outputs only)
+// e is 0/1, so a wave's part of x[h'] is a difference of popcounts of its
+// erasure ballot under the sign mask of j; (-1)^|h''&h| for h'' < NB <= 8
+// depends only on h mod NB = lane mod NB, so a wave's part of z is a lane
+// reduction over lane / NB followed by an NB-point transform across lanes
+// 0..NB-1.  Wave parts are added through LDS.  Integer sums (|sum| < 2^28)
+// reduced mod 65535 by folding (a result may be 65535 for 0: same residue,
+// and every consumer of the logs treats both alike); the last H_lo over the
+// NB output blocks is left to the decode passes (ework) or run by
+// fwht_lo_kernel.
+// (The kernel is short and runs once per CU: its time is instruction-fetch
+// bound, so it is written for few executed instructions, 4 waves sharing
+// each fetched line.)
+__device__ __forceinline__ uint32_t fold65535(uint32_t u) {
+    u = (u & 0xFFFFu) + (u >> 16);
+    return (u & 0xFFFFu) + (u >> 16);
 }
-__device__ __forceinline__ uint32_t mod65535(int v) {
-    const int r = v % 65535;
-    return (uint32_t)(r < 0 ? r + 65535 : r);
+__device__ __forceinline__ uint32_t mod65535(int v) { return fold65535((uint32_t)(v + 65535 * 4096)); }
+// (RS16_EVAL_ABL, timing-only builds: 3 = an empty kernel)
+#ifndef RS16_EVAL_ABL
+#define RS16_EVAL_ABL 0
+#endif
+#ifndef RS16_STAMPS
+#define RS16_STAMPS 0
+#endif
+// (RS16_STAMPS builds: slots as rs16_pass.hip's stamp(), 0 start, 1 flags
+// in, 2 sums done, 10 store issued, 11 store done, 14 / 15 real time)
+__device__ __forceinline__ void estamp(const ErasureSpec& e, int i) {
+#if RS16_STAMPS
+    if (e.stamps && threadIdx.x == 0) {
+        e.stamps[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
+        if (i == 0) {
+            e.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+            e.stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            e.stamps[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        }
+        if (i == 11) e.stamps[blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+    }
+#else
+    (void)e;
+    (void)i;
+#endif
 }
 template <int NB>
 __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const uint16_t* log_walsh, uint32_t* z) {
-    __shared__ int sh[NB][4];
-    const uint32_t j = blockIdx.x, t = threadIdx.x;
-    if (j < NB) decode_flags_block(e, j * 256u);
-    int v[NB];
-    const bool neg1 = __builtin_popcount(j & t) & 1;
+    __shared__ int part[2][4][NB];  // per-wave parts of x and z
+    __shared__ uint32_t words[8];   // block j's received bitmap (zero-tile flags)
+    const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (RS16_EVAL_ABL == 3) return;
+    estamp(e, 0);
+    const uint32_t lw = log_walsh[t * 256u + j];  // in flight from the start
+    // flag bytes of rows 256 h' + t, all loads issued before the first use
+    // (a row outside both segments reads a valid dummy byte)
+    uint32_t f[NB];
 #pragma unroll
-    for (int h = 0; h < NB; h++) {
-        const int x = (int)erasure_at(e, (uint32_t)h * 256u + t);
-        v[h] = neg1 ? -x : x;
+    for (int hp = 0; hp < NB; hp++) {
+        const uint32_t i = (uint32_t)hp * 256u + t;
+        const bool in_a = i < e.a_count && e.flags_a, in_b = i - e.chunk < e.b_count && e.flags_b;
+        const uint8_t* p = in_a ? e.flags_a + i : (in_b ? e.flags_b + (i - e.chunk) : (const uint8_t*)log_walsh);
+        f[hp] = *(const __attribute__((address_space(1))) uint8_t*)p;
     }
-    block_sum<NB>(v, sh);
+    const uint64_t sm = __ballot(__builtin_popcount(j & t) & 1);
+#pragma unroll
+    for (int hp = 0; hp < NB; hp++) {
+        // erasure_at / received_at with the flag byte already loaded
+        const uint32_t i = (uint32_t)hp * 256u + t;
+        const bool in_a = i < e.a_count, in_b = i - e.chunk < e.b_count;
+        const bool rcv = in_a ? (!e.flags_a || f[hp]) : (in_b && (!e.flags_b || f[hp]));
+        const bool era = in_a || in_b ? !rcv : (i < e.chunk ? e.pad_fill : e.tail_fill) != 0;
+        const uint64_t eb = __ballot(era);
+        if (lane == 0) part[0][wv][hp] = __popcll(eb & ~sm) - __popcll(eb & sm);
+        if ((uint32_t)hp == j) {
+            // workgroups j < NB: the pass metadata of block j (rows >= n
+            // lie past both segments: never received)
+            const uint64_t rb = __ballot(rcv);
+            if (lane == 0) {
+                words[2 * wv] = (uint32_t)rb;
+                words[2 * wv + 1] = (uint32_t)(rb >> 32);
+                if (e.rbits && i < e.n) {
+                    e.rbits[(i >> 5)] = (uint32_t)rb;
+                    e.rbits[(i >> 5) + 1] = (uint32_t)(rb >> 32);
+                }
+            }
+        }
+    }
+    estamp(e, 1);
+    __syncthreads();
+    if (j < NB && e.zflags) {
+        const uint32_t base = j * 256u, ts = 1u << e.zlo, ntile = e.n >> e.zlo;
+        if (t < 256u / ts && (base >> e.zlo) + t < ntile) {
+            bool any = false;
+            for (uint32_t r = t * ts; r < (t + 1) * ts; r += 32) {
+                const uint32_t m = ts >= 32 ? 0xFFFFFFFFu : ((1u << ts) - 1) << (r & 31);
+                any |= (words[r >> 5] & m) != 0;
+            }
+            e.zflags[(base >> e.zlo) + t] = any ? 0 : 1;
+        }
+    }
+    // y = sum_h' (-1)^|h&h'| x[h'] for h = t (h & h' = lane & h' for h' < 8)
     int y = 0;
 #pragma unroll
-    for (int h = 0; h < NB; h++) {
-        const int x = (int)mod65535(v[h]);
-        y += (__builtin_popcount(t & (uint32_t)h) & 1) ? -x : x;
+    for (int hp = 0; hp < NB; hp++) {
+        const int x = part[0][0][hp] + part[0][1][hp] + part[0][2][hp] + part[0][3][hp];
+        y += (__builtin_popcount(lane & (uint32_t)hp) & 1) ? -x : x;
     }
-    const int w = (int)(((uint64_t)mod65535(y) * log_walsh[t * 256u + j]) % GF_MODULUS);
+    int s = (int)fold65535(mod65535(y) * lw);
 #pragma unroll
-    for (int h = 0; h < NB; h++) v[h] = (__builtin_popcount(t & (uint32_t)h) & 1) ? -w : w;
-    block_sum<NB>(v, sh);
-    if (t < NB) {
-        int r = 0;
+    for (int off = NB; off < 64; off <<= 1) s += __shfl_xor(s, off);
 #pragma unroll
-        for (int h = 0; h < NB; h++)
-            if ((uint32_t)h == t) r = v[h];
-        z[t * 256u + j] = mod65535(r);
+    for (int d = 1; d < NB; d <<= 1) {
+        const int p = __shfl_xor(s, d);
+        s = (lane & d) ? p - s : s + p;
     }
+    if (lane < NB) part[1][wv][lane] = s;
+    estamp(e, 2);
+    __syncthreads();
+    if (t < NB) z[t * 256u + j] = mod65535(part[1][0][t] + part[1][1][t] + part[1][2][t] + part[1][3][t]);
+    estamp(e, 10);
+#if RS16_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    estamp(e, 11);
+#endif
 }
 
 hipError_t launch_eval_poly_small(const ErasureSpec& e, uint32_t n, uint32_t* work, uint32_t* out_elog,
-                                  const uint16_t* log_walsh, hipStream_t s) {
+                                  const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
     const uint32_t nb = n <= 256 ? 1 : n / 256;
     switch (nb) {
         case 1: hipLaunchKernelGGL(eval_small_kernel<1>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
@@ -331,8 +383,9 @@ hipError_t launch_eval_poly_small(const ErasureSpec& e, uint32_t n, uint32_t* wo
         case 8: hipLaunchKernelGGL(eval_small_kernel<8>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
         default: return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(nb), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
-                       nullptr);
+    if (last_lo)
+        hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(nb), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
+                           nullptr);
     return hipGetLastError();
 }
 // Engine-level fwht / eval_poly (the C ABI ops): the layers run in the

@@ -109,20 +109,29 @@ RS16_PROG(DEC_HALF_SINGLE, LD_GATHER_DEC, true, false, true, ST_RESTORE)
 #ifndef RS16_Q8
 #define RS16_Q8 32
 #endif
+// Row bits in registers at T = 5 (the passes of the n <= 2048 codecs, which
+// are latency-bound: 128 waves at 16 rows per thread): 3 = 8 rows per thread
+// and 16 quads per tile row, twice the waves, each with half the butterfly
+// chain; 4 = the 16-row geometry of the larger passes.
+#ifndef RS16_R5
+#define RS16_R5 3
+#endif
 template <int T> struct Geo {
-    static constexpr int R = T > 4 ? 4 : T;               // row bits held in registers
+    static constexpr int R = T > 4 ? (T == 5 ? RS16_R5 : 4) : T;  // row bits held in registers
     static constexpr int NR = 1 << R;                     // rows per thread (a row set)
     static constexpr int SETS = 1 << (T - R);             // row sets per tile
     // quads per tile row: PIPE: 4 waves per workgroup from T = 6 on
-    // (Q = 256 / SETS); else 32 (two 16-row sets per wave) from T = 5 on
-    static constexpr int Q = (RS16_PIPE && T >= 6) ? 256 / SETS : (T == 8 ? RS16_Q8 : (T > 4 ? 32 : 64));
+    // (Q = 256 / SETS); else 32 (two 16-row sets per wave) from T = 5 on,
+    // 16 (four 8-row sets per wave) at T = 5 with 8 rows per thread
+    static constexpr int Q = (RS16_PIPE && T >= 6) ? 256 / SETS
+                                                   : (T == 8 ? RS16_Q8 : (T > 4 ? (R == 3 ? 16 : 32) : 64));
     static constexpr int HWS = 64 / Q;                    // row sets per wave
     static constexpr int W = SETS / HWS > 0 ? SETS / HWS : 1;  // waves per workgroup
     static constexpr int SHB = T - R;                     // layout B: k = s + (m << SHB)
     static constexpr int THREADS = 64 * W;
     static constexpr int NTAB = (1 << T) - 1;             // twiddle groups per direction
-    // Tables of layers kb >= 4 (layout-B phase) come last: t >= TSPLIT.
-    static constexpr int TSPLIT = T > 4 ? (1 << T) - (1 << (T - 4)) : 0;
+    // Tables of layers kb >= R (layout-B phase) come last: t >= TSPLIT.
+    static constexpr int TSPLIT = T > 4 ? (1 << T) - (1 << (T - R)) : 0;
 };
 
 // The layout switch goes through the LDS image in one round (32 KiB at
@@ -590,13 +599,24 @@ struct NoFin {
 template <int T, bool LB, int KB0, int KB1, bool FFT> struct LayerSeq {
     static constexpr int SH = LB ? Geo<T>::SHB : 0;
     static constexpr int NR = Geo<T>::NR;
-    static constexpr bool DF = RS16_EARLY_ST && FFT && !LB && KB0 == 0 && KB1 == 4 && NR == 16;
-    // pre-order of the radix-16 group tree, (kb, gi) packed as kb * 16 + gi
+    static constexpr bool DF = RS16_EARLY_ST && FFT && !LB && KB0 == 0 && KB1 == Geo<T>::R && NR >= 8;
+    // pre-order of the group tree (node (kb, gi), children (kb-1, 2gi) and
+    // (kb-1, 2gi+1)), (kb, gi) packed as kb * 16 + gi; radix 16:
+    // (3,0) (2,0) (1,0) (0,0) (0,1) (1,1) (0,2) (0,3) (2,1) (1,2) ...
     static constexpr int df_at(int g) {
-        constexpr int ord[15] = {3 * 16 + 0, 2 * 16 + 0, 1 * 16 + 0, 0 * 16 + 0, 0 * 16 + 1, 1 * 16 + 1, 0 * 16 + 2,
-                                 0 * 16 + 3, 2 * 16 + 1, 1 * 16 + 2, 0 * 16 + 4, 0 * 16 + 5, 1 * 16 + 3, 0 * 16 + 6,
-                                 0 * 16 + 7};
-        return ord[g];
+        int skb[16] = {}, sgi[16] = {};
+        int sp = 0, n = 0;
+        skb[sp] = KB1 - 1, sgi[sp] = 0, sp++;
+        while (sp > 0) {
+            sp--;
+            const int kb = skb[sp], gi = sgi[sp];
+            if (n++ == g) return kb * 16 + gi;
+            if (kb > 0) {
+                skb[sp] = kb - 1, sgi[sp] = 2 * gi + 1, sp++;
+                skb[sp] = kb - 1, sgi[sp] = 2 * gi, sp++;
+            }
+        }
+        return 0;
     }
     static constexpr int kb_of(int s) { return FFT ? KB1 - 1 - s : KB0 + s; }
     static constexpr int groups_of(int s) { return NR >> (kb_of(s) - SH + 1); }
@@ -934,7 +954,8 @@ __device__ __forceinline__ void load_rows(const PassArgs& a, const Thr& c, uint3
         uint32_t bits;
         // (uni(): each word stays a scalar load; a select of two loads would
         // be folded into one per-lane vector load)
-        if constexpr (G::HWS == 4) bits = ((sub >> 1) ? uni(rb[1]) : uni(rb[0])) >> ((sub & 1) * 16);
+        if constexpr (NR == 8) bits = uni(rb[0]) >> ((row0 & 31) + sub * 8);  // (HWS * 8 <= 32 rows)
+        else if constexpr (G::HWS == 4) bits = ((sub >> 1) ? uni(rb[1]) : uni(rb[0])) >> ((sub & 1) * 16);
         else if constexpr (G::HWS == 2) bits = uni(rb[0]) >> (sub * 16);
         else bits = uni(rb[0]) >> (row0 & 31);
         bits &= (1u << NR) - 1;
@@ -980,7 +1001,14 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
     // Row r of this pass came from DEC_FIRST tile r >> lo = k + (b_high << T).
     // zrow bit m: this thread's (layout-A) row m is such a skipped, zero row;
     // zmask bit j: tile rows [16j, 16j+16) all are (uniform, scalar loads).
-    if constexpr (P == DEC_MID && T > 4) {
+    if constexpr (P == DEC_MID && T > 4 && R != 4) {
+        // (8-row sets: one flag byte per row, per lane; no zmask pruning)
+        if (a.zflags) {
+            const uint8_t* zt = a.zflags + (c.b_high << T) + (c.s << R);
+#pragma unroll
+            for (int m = 0; m < NR; m++) d.zrow |= (uint32_t)(zt[m] & 1u) << m;
+        }
+    } else if constexpr (P == DEC_MID && T > 4) {
         if (a.zflags) {
             const uint8_t* zt = a.zflags + (c.b_high << T);
             // the wave's HWS row sets are 16 * HWS consecutive flag bytes:
@@ -1268,7 +1296,8 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     constexpr int R = G::R;
     constexpr int NQR = Rnd<P, T>::NQR;
     constexpr bool TWO = SM::TWO;
-    constexpr bool ZERO_SKIP = P == DEC_MID && T > 4;  // DEC_MID runs with T >= 5 only
+    // (DEC_MID runs with T >= 5 only; the 16-row-block pruning needs R = 4)
+    constexpr bool ZERO_SKIP = P == DEC_MID && T > 4 && G::R == 4;
     // stores inside the last FFT block (one-item build, 16 rows per lane, not
     // the output-pruned DEC_MID; the reveal stores measured slower inside it)
     constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && !RS16_PIPE && P != DEC_MID && PT::STORE != ST_RESTORE &&
@@ -1323,7 +1352,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                 if constexpr (LateS2<P, T>::value) s3.commit((uint4*)(smem + SM::TAB1_OFF));
             });
             stamp(a, 4);
-            layers<T, true, 4, (T > 4 ? T : 4), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
+            layers<T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
                                                                                                 tab2, d.zmask);
             in_b = true;
         }
@@ -1339,7 +1368,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     // ---------------- FFT ----------------
     if constexpr (PT::FFT) {
         if constexpr (T > 4) {
-            layers<T, true, 4, (T > 4 ? T : 4), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
+            layers<T, true, R, (T > 4 ? T : R), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
             stamp(a, 7);
             prio<P, 3>();

@@ -8,7 +8,10 @@ duration of each phase of a workgroup (s_memtime cycles at the workgroup's
 own clock).  Phases (rs16_pass.hip stamp()): 0 start, 1 loads issued,
 2 tables staged, 3 first layout-A layers, 4 layout switch, 5 first
 direction done, 6 formal derivative, 7 layout-B FFT layers, 8 layout
-switch, 9 last layers, 10 stores issued, 11 stores done."""
+switch, 9 last layers, 10 stores issued, 11 stores done; EVAL_POLY (the
+n <= 2048 eval kernel, rs16_misc.hip): 0 start, 1 flags in, 2 sums done,
+10 store issued, 11 store done.  Programs: RS16_STAMP_PROGS (comma list);
+size: argv[1] (k = m)."""
 import ctypes as C
 import json
 import os
@@ -53,7 +56,8 @@ def main():
     err = RS16Error()
     out = {}
     raw = {}
-    for name in ["ENC_FIRST", "ENC_MID", "ENC_LAST", "DEC_HALF_FIRST", "DEC_HALF_MID", "DEC_HALF_LAST"]:
+    progs = os.environ.get("RS16_STAMP_PROGS", "ENC_FIRST,ENC_MID,ENC_LAST,DEC_HALF_FIRST,DEC_HALF_MID,DEC_HALF_LAST")
+    for name in progs.split(","):
         buf.upload(np.zeros(nwg * 16, np.uint64))
         lib().rs16_engine_set_stamps(eng.h, buf.ptr, names[name], C.byref(err))
         step()
