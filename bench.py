@@ -389,7 +389,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (ChaCha8 seed=rank stream of the reference benches; inputs resident in HBM)",
-            "config": {"workload": f"{k}:{m} x {S} B encode + 100%-loss decode per GPU (BASELINE configs[3])",
+            "config": {"workload": f"{k}:{m} x {S} B encode + 100%-loss decode per GPU" +
+                       (" (BASELINE configs[3])" if (k, m, S) == (32768, 32768, 1024) else
+                        " (BASELINE configs[1] + [2])" if (k, m, S) == (1000, 1000, 1024) else ""),
                        "original_count": k, "recovery_count": m, "shard_bytes": S,
                        "parallelism": f"independent stripes x {world} (weak, no collective)",
                        "column_slices": args.slices},
