@@ -341,6 +341,29 @@ def main():
                                      "decode_us": t1 / args.steps * 1e6, "lost_originals": L1,
                                      "received": f"originals 0..{k - L1}, recovery 0..{L1}"}
 
+    if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
+        # BASELINE configs[4] (32768:32768 x 64 KiB over 8 GPUs): one rank's
+        # share, an 8 KiB column slice of every shard, measured on this GPU
+        # (random bytes; the decode must restore every original)
+        S4 = 65536 // 8
+        o4 = np.random.default_rng(seed).integers(0, 256, (k, S4), dtype=np.uint8)
+        a4 = DeviceArray.from_numpy(eng, o4)
+        r4, x4 = DeviceArray(eng, m * S4), DeviceArray(eng, k * S4)
+        e4 = lambda: rs16.encode_device(k, m, S4, a4.ptr, r4.ptr, engine=eng)
+        d4 = lambda: rs16.decode_device(k, m, S4, x4.ptr, d_of.ptr, r4.ptr, d_rf.ptr, k - loss, loss, engine=eng)
+        e4()
+        d4()
+        assert np.array_equal(x4.download(shape=(k, S4)), o4), "configs[4] share: decode did not restore"
+        for _ in range(2):
+            e4(); d4()
+        n4 = max(3, args.steps // 4)
+        t4 = timed(lambda: (e4(), d4()), n4)
+        extra["configs4_rank_share"] = {
+            "workload": f"{k}:{m} x {S4} B encode + 100%-loss decode (one rank's column slice of configs[4])",
+            "gib_s": 2 * (k + m) * S4 * n4 / t4 / GIB, "ms_per_step": t4 / n4 * 1e3,
+            "x8_gpus_estimate_gib_s": 8 * 2 * (k + m) * S4 * n4 / t4 / GIB}
+        del a4, r4, x4
+
     if not args.no_extra:
         # Shards that start and end in host memory (north_star: recorded beside
         # the device-resident rate): rs16_encode_host / rs16_decode_host on

@@ -95,14 +95,15 @@ int rs16_engine_ifft(rs16_engine* eng, void* data, size_t shard_count, size_t sh
 int rs16_engine_ifft_skew_end(rs16_engine* eng, void* data, size_t shard_count, size_t shard_bytes, size_t pos,
                               size_t size, size_t truncated_size, void* stream, rs16_error* err);
 /* Engine::fwht (src/engine.rs:175) on a device u16[65536]; data beyond
- * truncated_size must be zero (the only way eval_poly uses it).  The
- * butterflies are exact in Z/65535 (ones' complement): an output equals the
- * reference's as a residue, and may read 65535 where the reference has 0 or
- * the reverse (both mean the same log, exp[65535] == exp[0],
- * src/engine/tables.rs:118). */
+ * truncated_size must be zero (the only way eval_poly uses it).  Bit-exact
+ * u16 outputs: the engine-level op runs the reference's layer order with its
+ * add_mod / sub_mod (src/engine.rs:90-100), so 0 and 65535 come out where the
+ * reference has them (tests/test_gpu_engine.py).  The decoders' internal
+ * erasure-log kernels only need the residue mod 65535 and use a faster order
+ * (both values mean the same log, exp[65535] == exp[0], src/engine/tables.rs:118). */
 int rs16_engine_fwht(rs16_engine* eng, uint16_t* d_data, size_t truncated_size, void* stream, rs16_error* err);
-/* Engine::eval_poly (src/engine.rs:207-218) on a device u16[65536]; same
- * residue convention as rs16_engine_fwht. */
+/* Engine::eval_poly (src/engine.rs:207-218) on a device u16[65536]; bit-exact
+ * as rs16_engine_fwht. */
 int rs16_engine_eval_poly(rs16_engine* eng, uint16_t* d_erasures, size_t truncated_size, void* stream,
                           rs16_error* err);
 /* Engine::mul (src/engine.rs:198): x[] *= log_m, bytes % 64 == 0. */
