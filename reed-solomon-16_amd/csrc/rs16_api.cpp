@@ -223,6 +223,7 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->ws_flags.release();
     e->ws_zflag.release();
     e->ws_rbits.release();
+    e->ws_lost.release();
     for (auto& sl : e->hslot) {
         if (sl.s) (void)hipStreamSynchronize(sl.s), (void)hipStreamDestroy(sl.s);
         sl.orig.release(), sl.rec.release(), sl.z.release(), sl.u.release();

@@ -284,6 +284,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     RS16_HIP(ws_elog.reserve(GF_ORDER * 4));
     RS16_HIP(ws_zflag.reserve(256));
     RS16_HIP(ws_rbits.reserve(GF_ORDER / 8));
+    RS16_HIP(ws_lost.reserve(256 * 8 + 16));
     ErasureSpec es;
     es.flags_a = flags_a;
     es.flags_b = flags_b;
@@ -299,6 +300,12 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.zflags = L > 8 ? (uint8_t*)ws_zflag.p : nullptr;
     es.n = g.n;
     es.zlo = (uint32_t)(L / 2);
+    // the lost originals' row range prunes the general multi-pass decode
+    // (the half-transform decode restores every original: not needed)
+    const bool prune = !half_decode(g) && L > 8;
+    es.lostpart = prune ? (uint32_t*)ws_lost.p : nullptr;
+    es.lostrange = prune ? (uint32_t*)ws_lost.p + 512 : nullptr;
+    es.orig_b = g.high ? 1 : 0;
     es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
@@ -388,6 +395,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     // One flag per DEC_FIRST tile (2^hi <= 256): tiles without a received
     // row are skipped by DEC_FIRST and read as zero by DEC_MID / DEC_LAST.
     a.zflags = (const uint8_t*)ws_zflag.p;
+    a.lostrange = (const uint32_t*)ws_lost.p + 512;  // (written by decode_eval)
     // Launch only the tiles that can hold a received row: a segment with no
     // received shard contributes none (its tiles are flagged by block 0).
     const uint32_t tile = 1u << lo, ntiles = 1u << hi;

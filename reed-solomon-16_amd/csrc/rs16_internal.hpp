@@ -112,6 +112,12 @@ struct PassArgs {
     // (launch_eval_poly_from_flags, last_lo = false): DEC_FIRST / DEC_LAST at
     // T = 8 finish it for their tile's rows in LDS.  nullptr: use elog.
     const uint32_t* ework;
+    // Lost originals' row range [lostrange[0], lostrange[1]) of a general
+    // decode, written by the eval_poly kernels from the received flags
+    // (nullptr: not pruned).  DEC_MID narrows [need_lo, need_hi) to the last
+    // pass's tiles that hold a lost original; DEC_LAST workgroups of other
+    // tiles return at once (their rows would only be stored if lost).
+    const uint32_t* lostrange;
     // diagnostic timeline buffer (RS16_STAMPS builds; nullptr otherwise)
     uint64_t* stamps;
 };
@@ -140,6 +146,14 @@ struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.r
     uint32_t* rbits;
     uint8_t* zflags;
     uint32_t n, zlo;
+    // Lost-original rows (rows of the originals' segment -- B when orig_b,
+    // else A -- without a received flag): lostpart[2 b], lostpart[2 b + 1] =
+    // the first / one past the last lost row of block b (~0u / 0 if none),
+    // reduced to lostrange[0..1] = [first lost row, last lost row + 1)
+    // ({~0u, 0} if none).  nullptr: not computed.
+    uint32_t* lostpart;
+    uint32_t* lostrange;
+    uint32_t orig_b;
     uint64_t* stamps;          // RS16_STAMPS builds: eval timeline (rs16_engine_set_stamps)
 };
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,

@@ -110,6 +110,41 @@ __device__ __forceinline__ bool received_at(const ErasureSpec& e, uint32_t i) {
     if (i >= e.chunk && i - e.chunk < e.b_count) return e.flags_b ? ((cu8p)e.flags_b)[i - e.chunk] != 0 : true;
     return false;
 }
+// Row i lies in the originals' segment (B for the high rate, A for the low).
+__device__ __forceinline__ bool orig_row(const ErasureSpec& e, uint32_t i) {
+    return e.orig_b ? (i >= e.chunk && i - e.chunk < e.b_count) : i < e.a_count;
+}
+// First / one past the last lost-original row of block blk (rows base +
+// 64 j + bit of lmask[j]), ~0u / 0 if none, by lane 0 of the wave.
+__device__ __forceinline__ void lost_part_wave(const ErasureSpec& e, uint32_t blk, uint32_t base,
+                                               const uint64_t (&lmask)[4]) {
+    uint32_t lo = ~0u, hi = 0;
+#pragma unroll
+    for (int j = 3; j >= 0; j--)
+        if (lmask[j]) lo = base + 64u * j + (uint32_t)__builtin_ctzll(lmask[j]);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (lmask[j]) hi = base + 64u * j + 64u - (uint32_t)__builtin_clzll(lmask[j]);
+    if ((threadIdx.x & 63) == 0) {
+        e.lostpart[2 * blk] = lo;
+        e.lostpart[2 * blk + 1] = hi;
+    }
+}
+// lostrange = [min lostpart lo, max lostpart hi) over the 256 blocks, by one wave.
+__device__ __forceinline__ void lost_range_wave(const ErasureSpec& e) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint4 p0 = ((const uint4*)e.lostpart)[2 * lane], p1 = ((const uint4*)e.lostpart)[2 * lane + 1];
+    uint32_t lo = min(min(p0.x, p0.z), min(p1.x, p1.z)), hi = max(max(p0.y, p0.w), max(p1.y, p1.w));
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, d));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, d));
+    }
+    if (lane == 0) {
+        e.lostrange[0] = lo;
+        e.lostrange[1] = hi;
+    }
+}
 // Received-row bitmap and zero-tile flags of rows [base, base + 256) by one
 // wave, from the ballots rmask[j] of rows base + 64 j + lane: rbits words,
 // zflags per tile of 2^zlo rows.
@@ -196,23 +231,27 @@ __device__ __forceinline__ void fwht256_wave(uint32_t (&v)[4]) {
 __global__ void __launch_bounds__(64) fwht_lo_flags_kernel(ErasureSpec e, uint32_t* out32) {
     const uint32_t base = blockIdx.x * 256u, lane = threadIdx.x;
     uint32_t v[4];
-    uint64_t rmask[4];
+    uint64_t rmask[4], lmask[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const uint32_t i = base + lane + 64u * j;
         v[j] = erasure_at(e, i);
-        rmask[j] = __ballot(i < e.n && received_at(e, i));
+        const bool rcv = i < e.n && received_at(e, i);
+        rmask[j] = __ballot(rcv);
+        lmask[j] = __ballot(i < e.n && orig_row(e, i) && !rcv);
     }
     block_flags_wave(e, base, rmask);
+    if (e.lostpart) lost_part_wave(e, blockIdx.x, base, lmask);
     fwht256_wave(v);
 #pragma unroll
     for (int j = 0; j < 4; j++) out32[base + lane + 64u * j] = v[j];
 }
 // Strided 256-point FWHT (row bits 8-15), x LogWalsh mod 65535, and again;
 // one wave per column.
-__global__ void __launch_bounds__(64) fwht_hi_mulw_kernel(const uint32_t* in32, uint32_t* out32,
+__global__ void __launch_bounds__(64) fwht_hi_mulw_kernel(ErasureSpec e, const uint32_t* in32, uint32_t* out32,
                                                           const uint16_t* log_walsh) {
     const uint32_t lane = threadIdx.x;
+    if (blockIdx.x == 0 && e.lostrange) lost_range_wave(e);
     uint32_t v[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) v[j] = in32[blockIdx.x + 256u * (lane + 64u * j)];
@@ -235,7 +274,7 @@ __global__ void __launch_bounds__(64) fwht_hi_mulw_kernel(const uint32_t* in32, 
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
     hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(64), 0, s, e, work);
-    hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(64), 0, s, work, work, log_walsh);
+    hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(64), 0, s, e, work, work, log_walsh);
     if (last_lo)
         hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
                            nullptr);
@@ -311,6 +350,8 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
         f[hp] = *(const __attribute__((address_space(1))) uint8_t*)p;
     }
     const uint64_t sm = __ballot(__builtin_popcount(j & t) & 1);
+    __shared__ uint32_t lpart[2][4];  // workgroup 0: per-wave lost-original row range
+    uint32_t wlo = ~0u, whi = 0;
 #pragma unroll
     for (int hp = 0; hp < NB; hp++) {
         // erasure_at / received_at with the flag byte already loaded
@@ -320,6 +361,14 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
         const bool era = in_a || in_b ? !rcv : (i < e.chunk ? e.pad_fill : e.tail_fill) != 0;
         const uint64_t eb = __ballot(era);
         if (lane == 0) part[0][wv][hp] = __popcll(eb & ~sm) - __popcll(eb & sm);
+        if (j == 0 && e.lostrange) {
+            const uint64_t lb = __ballot(orig_row(e, i) && !rcv);
+            const uint32_t r0 = (uint32_t)hp * 256u + wv * 64u;
+            if (lb) {
+                wlo = min(wlo, r0 + (uint32_t)__builtin_ctzll(lb));
+                whi = max(whi, r0 + 64u - (uint32_t)__builtin_clzll(lb));
+            }
+        }
         if ((uint32_t)hp == j) {
             // workgroups j < NB: the pass metadata of block j (rows >= n
             // lie past both segments: never received)
@@ -334,8 +383,16 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
             }
         }
     }
+    if (j == 0 && lane == 0) {
+        lpart[0][wv] = wlo;
+        lpart[1][wv] = whi;
+    }
     estamp(e, 1);
     __syncthreads();
+    if (j == 0 && t == 0 && e.lostrange) {
+        e.lostrange[0] = min(min(lpart[0][0], lpart[0][1]), min(lpart[0][2], lpart[0][3]));
+        e.lostrange[1] = max(max(lpart[1][0], lpart[1][1]), max(lpart[1][2], lpart[1][3]));
+    }
     if (j < NB && e.zflags) {
         const uint32_t base = j * 256u, ts = 1u << e.zlo, ntile = e.n >> e.zlo;
         if (t < 256u / ts && (base >> e.zlo) + t < ntile) {

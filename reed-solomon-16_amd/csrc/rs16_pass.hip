@@ -1486,6 +1486,14 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     uint32_t tile, slab;
     set_item(c, a, it0, G::Q, tile, slab);
 #if !RS16_PIPE
+    if constexpr (P == DEC_LAST) {
+        // A tile without a lost original stores nothing: return before any
+        // load (the decode's lost rows are [lostrange[0], lostrange[1])).
+        if (a.lostrange) {
+            const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
+            if (!((tile << T) < r1 && ((tile + 1) << T) > r0)) return;
+        }
+    }
     // one item per workgroup (launch_pass sets per_wg = 1): straight-line code
     // (a loop lets the compiler hoist per-row address terms out of it, which
     // costs more VGPRs than the 128 of four waves per SIMD).  The twiddle
@@ -1508,6 +1516,16 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     st.issue(a, c);  // twiddle tables first: they do not queue behind the tile
     ItemRegs<P, T> cur;
     load_item<P, T>(a, c, tile, cur);
+    if constexpr (P == DEC_MID) {
+        // Only the last pass's tiles that hold a lost original are consumed:
+        // tile row k = rows [k << lo, (k + 1) << lo) (read with the rows in flight)
+        if (a.lostrange) {
+            const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
+            const bool any = r0 < r1;
+            a.need_lo = max(a.need_lo, any ? r0 >> a.lo : 0u);
+            a.need_hi = min(a.need_hi, any ? ((r1 - 1) >> a.lo) + 1 : 0u);
+        }
+    }
     stamp(a, 1);
     prio<P, 0>();
     st.finish(a, c, smem);

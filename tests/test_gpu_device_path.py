@@ -214,3 +214,38 @@ def test_column_slices(eng, slices, k, m, sb):
         assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
     finally:
         eng.set_slices(1)
+
+
+def lost_pattern(k, m, pattern):
+    """Received masks whose lost originals sit in one part of the originals'
+    segment; recovery 0..lost given."""
+    om = np.ones(k, bool)
+    if pattern == "tail":      # benches/benchmarks.rs:84-87 (1 %): the last L originals
+        om[k - max(1, min(k, m) // 100):] = False
+    elif pattern == "head":
+        om[:3] = False
+    elif pattern == "two":     # the range spans (almost) the whole segment
+        om[[1, k - 2]] = False
+    elif pattern == "one_mid":
+        om[k // 2 + 5] = False
+    elif pattern == "edge":    # across a 256-row block boundary
+        om[250:262] = False
+    lost = int((~om).sum())
+    rm = np.zeros(m, bool)
+    rm[:lost] = True
+    return om, rm
+
+
+@pytest.mark.parametrize("pattern", ["tail", "head", "two", "one_mid", "edge"])
+@pytest.mark.parametrize("k,m,sb", [(32768, 32768, 64), (4096, 4096, 128), (2000, 2000, 64), (1000, 1000, 1024),
+                                    (3000, 30000, 64), (30000, 3000, 64), (700, 300, 128)])
+def test_decode_lost_range_pruning(eng, k, m, sb, pattern):
+    # The general decode prunes DEC_MID's FFT / stores and DEC_LAST's tiles to
+    # the lost originals' row range computed on the device by the eval_poly
+    # kernels (rs16_misc.hip lost_part_wave / lost_range_wave, eval_small);
+    # every lost original must still come back bit-exactly, and received
+    # originals must stay untouched.
+    original = generate_original(k, sb, 13)
+    recovery = dev_encode(eng, original, m)
+    om, rm = lost_pattern(k, m, pattern)
+    assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
