@@ -364,6 +364,42 @@ def main():
             "x8_gpus_estimate_gib_s": 8 * 2 * (k + m) * S4 * n4 / t4 / GIB}
         del a4, r4, x4
 
+    if not args.no_extra and world == 1:
+        # Serving mode (not the metric): two independent stripes per step, one
+        # per engine / stream, so that one stripe's load and store phases
+        # overlap the other's butterflies.  Both restorations are checked.
+        eng2 = rs16.Engine(local)
+        o2 = generate_original(k, S, 1)
+        a2, r2, x2 = DeviceArray.from_numpy(eng2, o2), DeviceArray(eng2, m * S), DeviceArray(eng2, k * S)
+        f2o, f2r = DeviceArray.from_numpy(eng2, of), DeviceArray.from_numpy(eng2, rf)
+        if loss < k:
+            x2.upload(o2)
+
+        def two():
+            encode()
+            rs16.encode_device(k, m, S, a2.ptr, r2.ptr, engine=eng2)
+            decode()
+            rs16.decode_device(k, m, S, x2.ptr, f2o.ptr, r2.ptr, f2r.ptr, k - loss, loss, engine=eng2)
+
+        two()
+        eng2.synchronize()
+        assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
+        for _ in range(args.warmup):
+            two()
+        eng.synchronize()
+        eng2.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            two()
+        eng.synchronize()
+        eng2.synchronize()
+        t2 = time.perf_counter() - t0
+        extra["two_stripes_two_streams"] = {
+            "gib_s": 2 * step_bytes * args.steps / t2 / GIB, "ms_per_two_stripes": t2 / args.steps * 1e3,
+            "note": "serving-mode throughput, two independent 32768:32768 x 1 KiB stripes in flight; not the metric"}
+        del a2, r2, x2, f2o, f2r
+        eng2.close()
+
     if not args.no_extra:
         # Shards that start and end in host memory (north_star: recorded beside
         # the device-resident rate): rs16_encode_host / rs16_decode_host on

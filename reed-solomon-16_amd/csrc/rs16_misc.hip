@@ -251,19 +251,25 @@ __global__ void __launch_bounds__(64) fwht_lo_flags_kernel(ErasureSpec e, uint32
 __global__ void __launch_bounds__(64) fwht_hi_mulw_kernel(ErasureSpec e, const uint32_t* in32, uint32_t* out32,
                                                           const uint16_t* log_walsh) {
     const uint32_t lane = threadIdx.x;
-    if (blockIdx.x == 0 && e.lostrange) lost_range_wave(e);
-    uint32_t v[4];
+    uint32_t v[4], lw[4];
+    // LogWalsh does not depend on the previous kernel: its loads go first
+#pragma unroll
+    for (int j = 0; j < 4; j++) lw[j] = log_walsh[blockIdx.x + 256u * (lane + 64u * j)];
 #pragma unroll
     for (int j = 0; j < 4; j++) v[j] = in32[blockIdx.x + 256u * (lane + 64u * j)];
     fwht256_wave(v);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const uint32_t idx = blockIdx.x + 256u * (lane + 64u * j);
-        v[j] = (uint32_t)(((uint64_t)v[j] * log_walsh[idx]) % GF_MODULUS);
+        // v, lw <= 65535: the product fits 32 bits; two folds reduce it mod
+        // 65535 (65535 may stand for 0: same residue)
+        uint32_t p = v[j] * lw[j];
+        p = (p & 0xFFFFu) + (p >> 16);
+        v[j] = (p & 0xFFFFu) + (p >> 16);
     }
     fwht256_wave(v);
 #pragma unroll
     for (int j = 0; j < 4; j++) out32[blockIdx.x + 256u * (lane + 64u * j)] = v[j];
+    if (blockIdx.x == 0 && e.lostrange) lost_range_wave(e);
 }
 
 // eval_poly(e) = FWHT(LogWalsh . FWHT(e)) with FWHT = H_lo H_hi (row bits 0-7
