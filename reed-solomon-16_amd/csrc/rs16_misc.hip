@@ -2,6 +2,8 @@
 // FWHT / eval_poly kernels of the MI355X GF(2^16) Reed-Solomon engine.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "rs16_internal.hpp"
 
 namespace rs16 {
@@ -277,10 +279,155 @@ __global__ void __launch_bounds__(64) fwht_hi_mulw_kernel(ErasureSpec e, const u
 // then the last H_lo.  With last_lo == false the last H_lo is left to the
 // consumer: the 65536-row decode passes (256-row tiles = one H_lo block each)
 // finish it per tile in LDS (rs16_pass.hip), saving a kernel.
+// One-kernel eval_poly for block-aligned segments (eval_fused_ok): workgroup
+// j computes column j of H_lo(e) for all 256 blocks itself -- thread t reads
+// block t's 256 flag bytes (16 x 16-byte loads, L2-resident after the first
+// workgroup of an XCD) and, e being 0/1, x[t] = sum_r (-1)^|j&r| e[256t + r];
+// for a flagged block (e = 1 - rcv)
+//   x = sum_r sign(j, r) - sum_r sign(j, r) rcv(r),  sum_r sign(j, r) = 256 [j == 0],
+// where the received part is a v_dot4_i32_i8 of the bytes' "nonzero" bits
+// (0x80 = -128 as i8) with the sign bytes of the dword -- then H_hi, x LogWalsh,
+// H_hi by wave 0 (exact integers, then Z/65535), as fwht_hi_mulw_kernel.
+// Wave 1 writes block j's pass metadata (rbits, zflags) like
+// fwht_lo_flags_kernel; workgroup 0 reduces the lost originals' row range.
+// One kernel instead of two (the second waited for the first's stores).
+__device__ __forceinline__ uint32_t nz80(uint32_t f) {  // 0x80 in every nonzero byte
+    return __builtin_amdgcn_bitop3_b32((f & 0x7F7F7F7Fu) + 0x7F7F7F7Fu, f, 0x80808080u, 0xA8);  // (a | b) & c
+}
+// Region of block t (rows [256 t, 256 t + 256)) -- host-checked to be one of:
+// 0 flags_a, 1 pad, 2 flags_b, 3 tail.
+__device__ __forceinline__ int block_region(const ErasureSpec& e, uint32_t base) {
+    if (base < e.a_count) return 0;
+    if (base < e.chunk) return 1;
+    if (base - e.chunk < e.b_count) return 2;
+    return 3;
+}
+__global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t* out32, const uint16_t* log_walsh) {
+    __shared__ int xs[256];
+    __shared__ uint32_t lr[2][4];
+    const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint32_t lw[4];
+    if (wv == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) lw[i] = log_walsh[(lane + 64u * i) * 256u + j];
+    }
+    // ---- x[t]: column j of H_lo(e) for block t ----
+    const uint32_t base = t * 256u;
+    const int reg = block_region(e, base);
+    const uint8_t* fl = nullptr;  // flag bytes of the block (nullptr: no flags, all received)
+    if (reg == 0 && e.flags_a) fl = e.flags_a + base;
+    if (reg == 2 && e.flags_b) fl = e.flags_b + (base - e.chunk);
+    const uint32_t fill = reg == 1 ? e.pad_fill : (reg == 3 ? e.tail_fill : 0u);
+    // all erased rows give 256 [j == 0]; received (flagged) rows are subtracted
+    const int all = (reg == 0 || reg == 2) ? (fl ? 1 : 0) : (int)fill;
+    int acc = 0;  // -128 * sum_r sign(j, r) rcv(r)
+    uint32_t lo = ~0u, hi = 0;  // lost rows of this block (workgroup 0, originals' segment)
+    const bool want_lost = j == 0 && e.lostrange && (e.orig_b ? reg == 2 : reg == 0) && fl;
+    if (fl) {
+        // sign bytes of a dword: byte b -> (-1)^|j & b|; dword q adds (-1)^|(j >> 2) & q|
+        uint32_t sp = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) sp |= ((__builtin_popcount(j & b) & 1) ? 0xFFu : 0x01u) << (8 * b);
+        const uint32_t sm = ~sp + 0x01010101u;  // bytewise negation of the +-1 bytes (no carries)
+        const uint4* p = (const uint4*)fl;
+        uint4 v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = p[i];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t q = 4u * i + c;
+                const uint32_t n = nz80(w[c]);
+                acc = __builtin_amdgcn_sdot4((int)n, (int)((__builtin_popcount((j >> 2) & q) & 1) ? sm : sp), acc,
+                                             false);
+                if (want_lost) {
+                    const uint32_t m = ~n & 0x80808080u;  // erased bytes
+                    if (m) {
+                        lo = min(lo, base + 4u * q + (uint32_t)(__builtin_ctz(m) >> 3));
+                        hi = base + 4u * q + (uint32_t)((31 - __builtin_clz(m)) >> 3) + 1u;
+                    }
+                }
+            }
+        }
+    }
+    xs[t] = (j == 0 ? 256 * all : 0) + (acc >> 7);
+    if (j == 0 && e.lostrange) {
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, d));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, d));
+        }
+        if (lane == 0) lr[0][wv] = lo, lr[1][wv] = hi;
+    }
+    // ---- wave 1: block j's received bitmap and zero-tile flags ----
+    if (wv == 1) {
+        const uint32_t b0 = j * 256u;
+        uint64_t rmask[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t r = b0 + lane + 64u * i;
+            rmask[i] = __ballot(r < e.n && received_at(e, r));
+        }
+        block_flags_wave(e, b0, rmask);
+    }
+    __syncthreads();
+    if (j == 0 && e.lostrange && t == 0) {
+        e.lostrange[0] = min(min(lr[0][0], lr[0][1]), min(lr[0][2], lr[0][3]));
+        e.lostrange[1] = max(max(lr[1][0], lr[1][1]), max(lr[1][2], lr[1][3]));
+    }
+    if (wv != 0) return;
+    // ---- wave 0: y = H_hi(x) exactly, w = y * LW mod 65535, z = H_hi(w) ----
+    int y[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) y[i] = xs[lane + 64 * i];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const bool up = lane & d;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int p = __shfl_xor(y[i], d);
+            y[i] = up ? p - y[i] : y[i] + p;
+        }
+    }
+    {
+        const int a = y[0] + y[1], b = y[0] - y[1], c = y[2] + y[3], d = y[2] - y[3];
+        y[0] = a + c, y[2] = a - c, y[1] = b + d, y[3] = b - d;
+    }
+    uint32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        // |y| <= 65536: y + 2 * 65535 >= 0, folded to [0, 65535]
+        uint32_t u = (uint32_t)(y[i] + 2 * 65535);
+        u = (u & 0xFFFFu) + (u >> 16);
+        u = (u & 0xFFFFu) + (u >> 16);
+        uint32_t p = u * lw[i];
+        p = (p & 0xFFFFu) + (p >> 16);
+        v[i] = (p & 0xFFFFu) + (p >> 16);
+    }
+    fwht256_wave(v);
+#pragma unroll
+    for (int i = 0; i < 4; i++) out32[(lane + 64u * i) * 256u + j] = v[i];
+}
+// Segment boundaries on 256-row blocks and 16-byte aligned flag arrays.
+static bool eval_fused_ok(const ErasureSpec& e) {
+    const auto al = [](const uint8_t* p) { return ((uintptr_t)p & 15) == 0; };
+    return e.a_count % 256 == 0 && e.chunk % 256 == 0 && e.b_count % 256 == 0 && al(e.flags_a) && al(e.flags_b);
+}
+
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
-    hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(64), 0, s, e, work);
-    hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(64), 0, s, e, work, work, log_walsh);
+    static const int mode = [] {  // RS16_EVAL_FUSED=0: always the two-kernel form
+        const char* v = std::getenv("RS16_EVAL_FUSED");
+        return v ? std::atoi(v) : 1;
+    }();
+    if (mode && eval_fused_ok(e)) {
+        hipLaunchKernelGGL(eval_fused_kernel, dim3(256), dim3(256), 0, s, e, work, log_walsh);
+    } else {
+        hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(64), 0, s, e, work);
+        hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(64), 0, s, e, work, work, log_walsh);
+    }
     if (last_lo)
         hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
                            nullptr);
