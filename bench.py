@@ -294,6 +294,25 @@ def main():
                 "algorithmic_bytes_per_launch": alg,
                 "whole_step_frac": round(step_bytes / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
 
+    # The passes are bound by VALU issue, not HBM: the
+    # same kernel against the VALU ceiling of this GF(2^16) butterfly (a quad
+    # of 4 elements = 30 VALU instructions: 12 v_perm_b32 lookups, 10 selector
+    # ops, 6 v_bitop3 XORs, 2 XORs), at 1024 SIMDs x 16 lanes x 2.4 GHz peak
+    # clock.  Algorithmic work = element-butterflies of the pass's layers.
+    chunk = 1 << (m - 1).bit_length()
+    L_e = chunk.bit_length() - 1
+    lo_e, hi_e = L_e // 2, L_e - L_e // 2
+    layers = {"ENC_FIRST": lo_e, "ENC_MID": 2 * hi_e, "ENC_LAST": lo_e, "DEC_HALF_FIRST": lo_e,
+              "DEC_HALF_MID": 2 * hi_e, "DEC_HALF_LAST": lo_e}.get(dom)
+    valu = None
+    if layers is not None and L_e > 8:
+        bfly = layers * (chunk // 2) * (S // 2)
+        peak = 1024 * 16 * 2.4e9 * 4 / 30
+        valu = {"bound": "valu", "kernel": dom, "achieved": round(bfly / dom_avg_s / 1e12, 3),
+                "peak": round(peak / 1e12, 3), "unit": "T element-butterflies/s", "frac": round(bfly / dom_avg_s / peak, 4),
+                "butterflies_per_launch": bfly,
+                "note": "ceiling of this kernel's multiply (30 VALU instructions per 4-element butterfly), not a vendor peak"}
+
     extra = {}
     if not args.no_extra and (k, m) != (1000, 1000):
         # BASELINE configs[1] / [2]: 1000:1000 x 1 KiB encode, decode at 100 % loss
@@ -457,6 +476,7 @@ def main():
             "encode_gib_s": round(world * (k + m) * S * args.steps / dt_e / GIB, 3),
             "decode_gib_s": round(world * (k + m) * S * args.steps / dt_d / GIB, 3),
             "roofline": roofline,
+            "valu_roofline": valu,
             "cpu_baseline": cpu,
             "kernels_us": {n: round(v["avg_us"], 2) for n, v in kernels.items()},
             "extra": extra,
