@@ -33,3 +33,43 @@ def test_sparse_eval_matches_oracle(n):
     got = sparse_eval(e, n)[:n]
     # 65535 and 0 are the same residue (exp[65535] = exp[0], src/engine/tables.rs:118)
     assert np.array_equal(got % 65535, want[:n].astype(np.int64) % 65535)
+
+
+def _nz80(f):
+    """rs16_misc.hip nz80: 0x80 in every nonzero byte of u32 words."""
+    return (((f & 0x7F7F7F7F) + 0x7F7F7F7F) | f) & 0x80808080
+
+
+def fused_column_x(flags, j):
+    """x[t] of eval_fused_kernel's workgroup j for all-flagged blocks: 256 [j == 0]
+    plus (v_dot4_i32_i8 of the nonzero bits (0x80 = -128) with the +-1 Walsh
+    sign bytes of each dword, accumulated) >> 7."""
+    words = flags.reshape(256, 64, 4).astype(np.uint32)
+    words = (words << np.array([0, 8, 16, 24], np.uint32)).sum(axis=2, dtype=np.uint64).astype(np.uint32)
+    n = _nz80(words)                                                   # [block, dword]
+    nb = ((n[..., None] >> np.array([0, 8, 16, 24], np.uint32)) & 0xFF).astype(np.int64)
+    nb = np.where(nb > 127, nb - 256, nb)                             # as signed bytes
+    sp = np.array([-1 if _POP[j & b] else 1 for b in range(4)], np.int64)
+    sq = np.array([-1 if _POP[(j >> 2) & q] else 1 for q in range(64)], np.int64)
+    acc = (nb * sp[None, None, :]).sum(axis=2) @ sq                    # per block
+    return (256 if j == 0 else 0) + (acc >> 7)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_fused_eval_formulation_matches_oracle(seed):
+    # e = 1 - received for a decode whose segments are whole 256-row blocks
+    # (eval_fused_ok); arbitrary nonzero flag bytes count as received
+    rng = np.random.default_rng(seed)
+    flags = rng.choice(np.array([0, 1, 2, 127, 128, 255], np.uint8), 65536, p=[0.4, 0.3, 0.1, 0.1, 0.05, 0.05])
+    flags[4096:8192] = 0
+    flags[8192:12288] = 1
+    e = (flags == 0).astype(np.uint16)
+    x = np.stack([fused_column_x(flags, j) for j in range(256)], axis=1)  # [t, j] = H_lo(e) of block t, column j
+    assert np.array_equal(x, e.astype(np.int64).reshape(256, 256) @ SIGN.T)
+    lw = O.table("log_walsh").astype(np.int64).reshape(256, 256)
+    y = (SIGN @ x) % 65535                       # exact integers, then Z/65535
+    z = (SIGN @ ((y * lw) % 65535)) % 65535
+    got = ((z @ SIGN.T) % 65535).reshape(-1)
+    want = e.copy()
+    O.eval_poly(want, 65536)
+    assert np.array_equal(got % 65535, want.astype(np.int64) % 65535)
