@@ -322,13 +322,19 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
     const int all = (reg == 0 || reg == 2) ? (fl ? 1 : 0) : (int)fill;
     int acc = 0;  // -128 * sum_r sign(j, r) rcv(r)
     uint32_t lo = ~0u, hi = 0;  // lost rows of this block (workgroup 0, originals' segment)
-    const bool want_lost = j == 0 && e.lostrange && (e.orig_b ? reg == 2 : reg == 0) && fl;
     if (fl) {
-        // sign bytes of a dword: byte b -> (-1)^|j & b|; dword q adds (-1)^|(j >> 2) & q|
+        // sign bytes of a dword: byte b -> (-1)^|j & b|; dword q adds
+        // (-1)^|(j >> 2) & q| = bit q of the Walsh row wm (XOR of the bit
+        // patterns of the set bits of j >> 2)
         uint32_t sp = 0;
 #pragma unroll
         for (int b = 0; b < 4; b++) sp |= ((__builtin_popcount(j & b) & 1) ? 0xFFu : 0x01u) << (8 * b);
         const uint32_t sm = ~sp + 0x01010101u;  // bytewise negation of the +-1 bytes (no carries)
+        constexpr uint64_t PAT[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull, 0xF0F0F0F0F0F0F0F0ull,
+                                     0xFF00FF00FF00FF00ull, 0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
+        uint64_t wm = 0;
+#pragma unroll
+        for (int b = 0; b < 6; b++) wm ^= ((j >> (2 + b)) & 1) ? PAT[b] : 0ull;
         const uint4* p = (const uint4*)fl;
         uint4 v[16];
 #pragma unroll
@@ -337,16 +343,21 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
         for (int i = 0; i < 16; i++) {
             const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const uint32_t q = 4u * i + c;
-                const uint32_t n = nz80(w[c]);
-                acc = __builtin_amdgcn_sdot4((int)n, (int)((__builtin_popcount((j >> 2) & q) & 1) ? sm : sp), acc,
-                                             false);
-                if (want_lost) {
-                    const uint32_t m = ~n & 0x80808080u;  // erased bytes
+            for (int c = 0; c < 4; c++)
+                acc = __builtin_amdgcn_sdot4((int)nz80(w[c]), (int)(((wm >> (4 * i + c)) & 1) ? sm : sp), acc, false);
+        }
+        if (j == 0 && e.lostrange) {  // (uniform: workgroup 0 of a general decode)
+            const bool want = e.orig_b ? reg == 2 : reg == 0;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t m = want ? ~nz80(w[c]) & 0x80808080u : 0u;  // erased bytes
+                    const uint32_t r = base + 4u * (4 * i + c);
                     if (m) {
-                        lo = min(lo, base + 4u * q + (uint32_t)(__builtin_ctz(m) >> 3));
-                        hi = base + 4u * q + (uint32_t)((31 - __builtin_clz(m)) >> 3) + 1u;
+                        lo = min(lo, r + (uint32_t)(__builtin_ctz(m) >> 3));
+                        hi = r + (uint32_t)((31 - __builtin_clz(m)) >> 3) + 1u;
                     }
                 }
             }
