@@ -1486,6 +1486,11 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     uint32_t tile, slab;
     set_item(c, a, it0, G::Q, tile, slab);
 #if !RS16_PIPE
+    if constexpr (P == DEC_FIRST) {
+        // a tile without received rows is skipped (process_item): return
+        // before its table staging and row loads, so its slot frees at once
+        if (a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u)) return;
+    }
     if constexpr (P == DEC_LAST) {
         // A tile without a lost original stores nothing: return before any
         // load (the decode's lost rows are [lostrange[0], lostrange[1])).
