@@ -377,10 +377,12 @@ def main():
             e4(); d4()
         n4 = max(3, args.steps // 4)
         t4 = timed(lambda: (e4(), d4()), n4)
-        extra["configs4_rank_share"] = {
-            "workload": f"{k}:{m} x {S4} B encode + 100%-loss decode (one rank's column slice of configs[4])",
-            "gib_s": 2 * (k + m) * S4 * n4 / t4 / GIB, "ms_per_step": t4 / n4 * 1e3,
-            "x8_gpus_estimate_gib_s": 8 * 2 * (k + m) * S4 * n4 / t4 / GIB}
+        # (timed(): barrier + max over ranks; at 8 ranks this is configs[4] itself)
+        extra["configs4_column_slices"] = {
+            "workload": f"{k}:{m} x 65536 B split into 8 column slices of {S4} B (BASELINE configs[4]); "
+                        f"{world} slice(s) here, one per rank, encode + 100%-loss decode, no collective",
+            "gib_s": world * 2 * (k + m) * S4 * n4 / t4 / GIB, "per_rank_gib_s": 2 * (k + m) * S4 * n4 / t4 / GIB,
+            "ms_per_step": t4 / n4 * 1e3, "whole_configs4": world == 8}
         del a4, r4, x4
 
     if not args.no_extra and world == 1:
