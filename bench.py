@@ -178,7 +178,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     dist = None
+    json_fd = None
     if world > 1:
+        # gloo prints its connection messages on stdout: keep fd 1 for the
+        # one JSON line of rank 0 and send everything else to stderr
+        sys.stdout.flush()
+        json_fd = os.dup(1)
+        os.dup2(2, 1)
         import torch.distributed as dist  # control plane only (barrier, max of times)
         dist.init_process_group("gloo", init_method="env://")
 
@@ -484,7 +490,10 @@ def main():
             "extra": extra,
             "verified": verified,
         }
-        print(json.dumps(out), flush=True)
+        if json_fd is None:
+            print(json.dumps(out), flush=True)
+        else:
+            os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 
