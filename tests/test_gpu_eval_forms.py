@@ -61,3 +61,32 @@ def test_eval_forms_restore(fused):
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1]
     for k, m, pattern, ok in json.loads(line[7:]):
         assert ok, (k, m, pattern)
+
+
+def test_unaligned_flag_arrays():
+    # received-flag arrays at odd device addresses: eval_fused_ok refuses the
+    # one-kernel form (16-byte loads) and the two-kernel form runs instead
+    import numpy as np
+    import rs16
+    from rs16.device import DeviceArray
+    from rs16.util import generate_original
+
+    eng = rs16.default_engine()
+    k = m = 4096
+    sb = 128
+    orig = generate_original(k, sb, 3)
+    d_o, d_r = DeviceArray.from_numpy(eng, orig), DeviceArray(eng, m * sb)
+    rs16.encode_device(k, m, sb, d_o.ptr, d_r.ptr, engine=eng)
+    for lost_n in (k, 40):
+        om = np.ones(k, bool)
+        om[k - lost_n:] = False
+        rm = np.zeros(m, bool)
+        rm[:lost_n] = True
+        fo = np.concatenate([[7], om.astype(np.uint8)]).astype(np.uint8)  # flags start at byte 1
+        fr = np.concatenate([[7], rm.astype(np.uint8)]).astype(np.uint8)
+        d_fo, d_fr = DeviceArray.from_numpy(eng, fo), DeviceArray.from_numpy(eng, fr)
+        holes = orig.copy()
+        holes[~om] = 0
+        d_x = DeviceArray.from_numpy(eng, holes)
+        rs16.decode_device(k, m, sb, d_x.ptr, d_fo.ptr + 1, d_r.ptr, d_fr.ptr + 1, int(om.sum()), lost_n, engine=eng)
+        assert np.array_equal(d_x.download(shape=(k, sb)), orig), lost_n
