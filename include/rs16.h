@@ -24,7 +24,8 @@
  *    call when that was issued on another stream, so two streams never
  *    share the scratch concurrently (calls on one engine serialise; use one
  *    engine per stream for concurrent codecs).
- *  - rs16_engine_free synchronises the device, releases the work space of
+ *  - rs16_engine_free waits for the engine's work (its own streams and the
+ *    last caller stream it ran on, through an event), releases the work space of
  *    every encoder/decoder created on the engine and detaches them: a
  *    detached encoder/decoder fails every call with RS16_INVALID_ARGUMENT,
  *    and rs16_{en,de}coder_free of it only frees its host memory (safe in
@@ -139,18 +140,30 @@ rs16_encoder* rs16_encoder_new(rs16_engine* eng, int rate, size_t original_count
 void rs16_encoder_free(rs16_encoder* enc);
 int rs16_encoder_reset(rs16_encoder* enc, size_t original_count, size_t recovery_count, size_t shard_bytes,
                        rs16_error* err);
-/* add_original_shard (src/rate/encoder_work.rs:49-69); shard in host memory. */
+/* add_original_shard (src/rate/encoder_work.rs:49-69); shard in host memory.
+ * The shard is copied (host memcpy, no device call) into a page-locked image
+ * of the work buffer; consecutive shards stream to HBM in 1 MiB DMA copies
+ * while the caller keeps adding, so the caller may reuse its buffer at once. */
 int rs16_encoder_add_original_shard(rs16_encoder* enc, const void* shard, size_t len, rs16_error* err);
 /* same, shard in device memory (copied on the engine stream). */
 int rs16_encoder_add_original_shard_device(rs16_encoder* enc, const void* d_shard, size_t len, rs16_error* err);
 /* encode (rate_high.rs:44-83 / rate_low.rs:44-83); on success the
  * EncoderResult (src/encoder_result.rs) is valid until rs16_encoder_result_drop.
+ * Returns once the work is enqueued on the engine stream: the last staged
+ * rows go to HBM, the passes run, and when any original came from host
+ * memory the recovery rows come back in one DMA copy to page-locked memory
+ * (rs16_encoder_recovery waits for it).
  * The encode works in place: calling it again while the result is held
  * returns RS16_INVALID_ARGUMENT (the reference's &mut borrow makes that a
  * compile error, src/rate.rs:157-166); add_original_shard in that state
  * returns TooManyOriginalShards, as every original is in. */
 int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err);
-/* EncoderResult::recovery (src/encoder_result.rs:16-19): device pointer, NULL if index >= recovery_count. */
+/* EncoderResult::recovery (src/encoder_result.rs:16-19): host pointer to
+ * recovery shard `index` (shard_bytes, page-locked, valid until the result is
+ * dropped), NULL if index >= recovery_count (or on a device error, err set).
+ * The first call waits for the recovery rows to be in host memory. */
+const void* rs16_encoder_recovery(rs16_encoder* enc, size_t index, rs16_error* err);
+/* The same shard in HBM: device pointer, NULL if index >= recovery_count. */
 const void* rs16_encoder_recovery_device(rs16_encoder* enc, size_t index);
 /* Copy recovery shard `index` to host memory; returns 1 if it exists, 0 if not, <0 on error. */
 int rs16_encoder_recovery_copy(rs16_encoder* enc, size_t index, void* dst, size_t len, rs16_error* err);
@@ -166,7 +179,9 @@ rs16_decoder* rs16_decoder_new(rs16_engine* eng, int rate, size_t original_count
 void rs16_decoder_free(rs16_decoder* dec);
 int rs16_decoder_reset(rs16_decoder* dec, size_t original_count, size_t recovery_count, size_t shard_bytes,
                        rs16_error* err);
-/* add_original_shard / add_recovery_shard (src/rate/decoder_work.rs:62-116). */
+/* add_original_shard / add_recovery_shard (src/rate/decoder_work.rs:62-116).
+ * Host shards are staged like the encoder's (page-locked image of the work
+ * layout, runs of consecutive positions streamed to HBM while adding). */
 int rs16_decoder_add_original_shard(rs16_decoder* dec, size_t index, const void* shard, size_t len, rs16_error* err);
 int rs16_decoder_add_recovery_shard(rs16_decoder* dec, size_t index, const void* shard, size_t len, rs16_error* err);
 int rs16_decoder_add_original_shard_device(rs16_decoder* dec, size_t index, const void* d_shard, size_t len,
@@ -177,7 +192,13 @@ int rs16_decoder_add_recovery_shard_device(rs16_decoder* dec, size_t index, cons
  * The decode restores in place: decode or add_*_shard while the result is
  * held returns RS16_INVALID_ARGUMENT (a compile error in the reference). */
 int rs16_decoder_decode(rs16_decoder* dec, rs16_error* err);
-/* DecoderResult::restored_original (src/decoder_result.rs:16-19): device pointer or NULL. */
+/* DecoderResult::restored_original (src/decoder_result.rs:16-19): host
+ * pointer to restored original `index` (page-locked, valid until the result
+ * is dropped), NULL if it was received or index >= original_count (or on a
+ * device error, err set).  After a decode with host shards the restored rows
+ * come back in one DMA copy; the first call waits for it. */
+const void* rs16_decoder_restored_original(rs16_decoder* dec, size_t index, rs16_error* err);
+/* The same shard in HBM: device pointer or NULL. */
 const void* rs16_decoder_restored_original_device(rs16_decoder* dec, size_t index);
 /* Copy restored original `index` to host; returns 1 if restored, 0 if None, <0 on error. */
 int rs16_decoder_restored_original_copy(rs16_decoder* dec, size_t index, void* dst, size_t len, rs16_error* err);
@@ -264,6 +285,16 @@ int rs16_prog_count(void);
  * builds accept the call and record nothing. */
 int rs16_engine_set_stamps(rs16_engine* eng, void* d_buf, int prog, rs16_error* err);
 const char* rs16_prog_name(int prog);
+
+/* Diagnostics: process-wide switches to alternative code paths, for tests
+ * and measurements only (results are identical; 0 = the shipped paths).
+ * Returns the previous flags.  Not thread-safe against concurrent calls. */
+enum {
+    RS16_DIAG_FORCE_VOFF64 = 1,    /* 64-bit per-lane HBM offsets in every pass */
+    RS16_DIAG_EVAL_TWO_KERNEL = 2, /* eval_poly: the two-kernel form everywhere */
+    RS16_DIAG_EVAL_FULL = 4        /* eval_poly: the full 65536-point form for n <= 2048 */
+};
+int rs16_set_diagnostics(int flags);
 
 /* Diagnostics: host-side evaluation of the device multiply (same v_perm
  * byte-table format and code path as the kernels, with v_perm emulated):

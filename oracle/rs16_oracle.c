@@ -726,3 +726,60 @@ const uint16_t *oracle_table(int which) {
     default: return NULL;
     }
 }
+
+/* ------------------------------------------------------------------ */
+/* CPU baseline loop -- benches/benchmarks.rs:60-109 (benchmarks_main) */
+/* ------------------------------------------------------------------ */
+/* One benchmark row of the reference's `main` group, timed the way its
+ * b.iter closures run, with the restated engine `engine` behind the
+ * DefaultRate encoder/decoder (ReedSolomonEncoder / ReedSolomonDecoder):
+ *   loss_percent < 0: add_original_shard x k + encode          (:71-76)
+ *   else: L = min(k, m) * loss_percent / 100; add_original_shard(i) for
+ *         i < k - L, add_recovery_shard(i) for i < L, decode     (:84-107)
+ * `original` holds k shards, `recovery` m shards (S bytes each, contiguous).
+ * Iterations run until min_seconds have passed (at least one); returns the
+ * iteration count and the elapsed seconds.  Used only by bench.py's
+ * cpu_baseline leg. */
+#include <time.h>
+static double oracle_now(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+int oracle_bench_main(int engine, size_t k, size_t m, size_t S, const uint8_t *original, const uint8_t *recovery,
+                      int loss_percent, double min_seconds, size_t *iters, double *seconds) {
+    oracle_error err;
+    size_t n = 0;
+    double t0 = oracle_now(), t = 0.0;
+    if (loss_percent < 0) {
+        oracle_encoder *e = oracle_encoder_new(0, engine, k, m, S, &err);
+        if (!e) return err.code ? err.code : -1;
+        do {
+            for (size_t i = 0; i < k; i++)
+                if (oracle_encoder_add_original_shard(e, original + i * S, S, &err)) return err.code;
+            if (oracle_encoder_encode(e, &err)) return err.code;
+            oracle_encoder_reset_received(e); /* EncoderResult dropped */
+            n++;
+            t = oracle_now() - t0;
+        } while (t < min_seconds);
+        oracle_encoder_free(e);
+    } else {
+        const size_t loss = (k < m ? k : m) * (size_t)loss_percent / 100;
+        oracle_decoder *d = oracle_decoder_new(0, engine, k, m, S, &err);
+        if (!d) return err.code ? err.code : -1;
+        do {
+            for (size_t i = 0; i < k - loss; i++)
+                if (oracle_decoder_add_original_shard(d, i, original + i * S, S, &err)) return err.code;
+            for (size_t i = 0; i < loss; i++)
+                if (oracle_decoder_add_recovery_shard(d, i, recovery + i * S, S, &err)) return err.code;
+            if (oracle_decoder_decode(d, &err)) return err.code;
+            oracle_decoder_reset_received(d); /* DecoderResult dropped */
+            n++;
+            t = oracle_now() - t0;
+        } while (t < min_seconds);
+        oracle_decoder_free(d);
+    }
+    *iters = n;
+    *seconds = t;
+    return 0;
+}

@@ -106,6 +106,11 @@ extern "C" int rs16_engine_set_slices(rs16_engine* e, int n, rs16_error* err) {
     e->slices = n;
     return set_error(err, RS16_OK);
 }
+extern "C" int rs16_set_diagnostics(int flags) {
+    const int old = g_diag;
+    g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL);
+    return old;
+}
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
 extern "C" const char* rs16_prog_name(int prog) {
     static const char* names[] = {"GEN_FFT",   "GEN_IFFT",   "ENC_FIRST",     "ENC_MID",
@@ -212,7 +217,15 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
 extern "C" void rs16_engine_free(rs16_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
-    (void)hipDeviceSynchronize();  // every stream that used the engine's scratch or its children's work
+    // The streams this engine's work can be on: its own, the slice and
+    // host-pipeline streams, and the last caller stream that used its scratch
+    // (through order_ev).  Other engines and unrelated work are not waited for.
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (int j = 0; j < rs16_engine::MAX_SLICES; j++)
+        if (e->sl_own[j]) (void)hipStreamSynchronize(e->sl_own[j]);
+    for (auto& sl : e->hslot)
+        if (sl.s) (void)hipStreamSynchronize(sl.s);
+    if (e->last == rs16_engine::LAST_CALLER && e->order_ev) (void)hipEventSynchronize(e->order_ev);
     for (rs16_encoder* c : e->encoders) detach(c);
     for (rs16_decoder* c : e->decoders) detach(c);
     e->ws_z.release();
@@ -292,6 +305,7 @@ extern "C" int rs16_engine_fwht(rs16_engine* e, uint16_t* d, size_t trunc, void*
     if (int rc = e->order(e->pick(stream), err)) return rc;
     RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
     RS16_HIP(launch_fwht_u16(d, (uint32_t*)e->ws_work32.p, e->pick(stream)));
+    if (int rc = e->scratch_done(e->pick(stream), err)) return rc;
     return set_error(err, RS16_OK);
 }
 extern "C" int rs16_engine_eval_poly(rs16_engine* e, uint16_t* d, size_t trunc, void* stream, rs16_error* err) {
@@ -300,6 +314,7 @@ extern "C" int rs16_engine_eval_poly(rs16_engine* e, uint16_t* d, size_t trunc, 
     if (int rc = e->order(e->pick(stream), err)) return rc;
     RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
     RS16_HIP(launch_eval_poly_u16(d, (uint32_t*)e->ws_work32.p, e->d_log_walsh, e->pick(stream)));
+    if (int rc = e->scratch_done(e->pick(stream), err)) return rc;
     return set_error(err, RS16_OK);
 }
 extern "C" int rs16_engine_mul(rs16_engine* e, void* x, size_t bytes, uint16_t log_m, void* stream, rs16_error* err) {
@@ -330,8 +345,23 @@ extern "C" int rs16_engine_formal_derivative(rs16_engine* e, void* data, size_t 
     RS16_HIP(e->ws_fd.reserve(n * S));
     RS16_HIP(launch_formal_derivative((uint8_t*)e->ws_fd.p, (const uint8_t*)data, n, S, s));
     RS16_HIP(hipMemcpyAsync(data, e->ws_fd.p, n * S, hipMemcpyDeviceToDevice, s));
+    if (int rc = e->scratch_done(s, err)) return rc;
     return set_error(err, RS16_OK);
 }
+
+// ---------------------------------------------------------------------------
+// Host staging of the Rate-level API.  The reference copies every added shard
+// into its work buffer (src/rate/encoder_work.rs:49-69,
+// src/rate/decoder_work.rs:62-116) and serves results out of it
+// (EncoderResult::recovery / DecoderResult::restored_original).  Here a shard
+// added from host memory is copied (host memcpy, no HIP call) into a
+// page-locked image of the work buffer; runs of consecutive rows stream to
+// HBM in DMA copies of >= STREAM_BYTES while the caller keeps adding, the
+// rest goes at encode()/decode(); the results come back in one DMA copy into
+// the page-locked image, and the result accessors wait for it.  encode() and
+// decode() return once everything is enqueued on the engine stream.
+// ---------------------------------------------------------------------------
+static constexpr size_t STREAM_BYTES = (size_t)1 << 20;
 
 // ---------------------------------------------------------------------------
 // Encoder -- EncoderWork (src/rate/encoder_work.rs) + Rate encoders.
@@ -347,13 +377,35 @@ struct rs16_encoder {
     bool encoded = false;
     size_t k = 0, m = 0, S = 0, work_count = 0, received = 0;
     DevBuf work;
+    // Host staging: h_in holds the rows added from host memory (row = the
+    // shard's position, as the reference's work buffer); rows [run0,
+    // received) are there but not yet copied to `work`.  h_out receives the
+    // recovery rows.  in_done: the last H2D out of h_in (h_in may be
+    // rewritten once it completed); out_done: the D2H into h_out.
+    HostBuf h_in, h_out;
+    size_t run0 = 0;
+    bool host_round = false;  // a shard of this round came from host memory
+    bool out_on_host = false;  // the D2H of this round's recovery rows is issued
+    Pending in_done, out_done;
 };
 
 static void detach(rs16_encoder* enc) {
     enc->work.release();
+    enc->h_in.release();
+    enc->h_out.release();
+    enc->in_done.release();
+    enc->out_done.release();
     enc->eng = nullptr;
 }
 template <class V, class T> static void forget(V& v, T* x) { v.erase(std::remove(v.begin(), v.end(), x), v.end()); }
+
+static void encoder_new_round(rs16_encoder* enc) {
+    enc->received = 0;
+    enc->encoded = false;
+    enc->run0 = 0;
+    enc->host_round = false;
+    enc->out_on_host = false;
+}
 
 static int encoder_reset_impl(rs16_encoder* enc, size_t k, size_t m, size_t S, rs16_error* err) {
     if (!enc->eng) return set_error(err, RS16_INVALID_ARGUMENT);
@@ -367,8 +419,7 @@ static int encoder_reset_impl(rs16_encoder* enc, size_t k, size_t m, size_t S, r
     enc->m = m;
     enc->S = S;
     enc->work_count = wc;
-    enc->received = 0;
-    enc->encoded = false;
+    encoder_new_round(enc);
     return set_error(err, RS16_OK);
 }
 
@@ -390,7 +441,7 @@ extern "C" void rs16_encoder_free(rs16_encoder* enc) {
     if (rs16_engine* e = enc->eng) {
         (void)hipSetDevice(e->device);
         (void)hipStreamSynchronize(e->stream);
-        enc->work.release();
+        detach(enc);
         forget(e->encoders, enc);
     }
     delete enc;
@@ -398,16 +449,39 @@ extern "C" void rs16_encoder_free(rs16_encoder* enc) {
 extern "C" int rs16_encoder_reset(rs16_encoder* enc, size_t k, size_t m, size_t S, rs16_error* err) {
     return encoder_reset_impl(enc, k, m, S, err);
 }
+// Copy the staged host rows [run0, upto) to the device work rows.
+static int encoder_stream(rs16_encoder* enc, size_t upto, rs16_error* err) {
+    if (upto <= enc->run0) return RS16_OK;
+    const size_t S = enc->S;
+    RS16_HIP(hipMemcpyAsync((uint8_t*)enc->work.p + enc->run0 * S, (const uint8_t*)enc->h_in.p + enc->run0 * S,
+                            (upto - enc->run0) * S, hipMemcpyHostToDevice, enc->eng->stream));
+    enc->run0 = upto;
+    return RS16_OK;
+}
 static int encoder_add(rs16_encoder* enc, const void* shard, size_t len, bool device, rs16_error* err) {
     if (!enc->eng) return set_error(err, RS16_INVALID_ARGUMENT);
     if (enc->received == enc->k) return set_error(err, RS16_TOO_MANY_ORIGINAL_SHARDS, enc->k);
     if (len != enc->S) return set_error(err, RS16_DIFFERENT_SHARD_SIZE, enc->S, len);
-    if (int rc = enc->eng->activate(err)) return rc;
-    uint8_t* dst = (uint8_t*)enc->work.p + enc->received * enc->S;
-    if (device) RS16_HIP(hipMemcpyAsync(dst, shard, len, hipMemcpyDeviceToDevice, enc->eng->stream));
-    else RS16_HIP(hipMemcpyAsync(dst, shard, len, hipMemcpyHostToDevice, enc->eng->stream));
-    if (!device) RS16_HIP(hipStreamSynchronize(enc->eng->stream));  // the caller may reuse its buffer
-    enc->received++;
+    const size_t r = enc->received, S = enc->S;
+    if (device) {
+        if (int rc = enc->eng->activate(err)) return rc;
+        if (int rc = encoder_stream(enc, r, err)) return rc;  // (host rows before it)
+        RS16_HIP(hipMemcpyAsync((uint8_t*)enc->work.p + r * S, shard, len, hipMemcpyDeviceToDevice, enc->eng->stream));
+        enc->run0 = r + 1;
+    } else {
+        if (r == 0) {
+            // the previous round's copies out of h_in must be done
+            RS16_HIP(enc->in_done.wait());
+            RS16_HIP(enc->h_in.reserve(enc->k * S));
+        }
+        memcpy((uint8_t*)enc->h_in.p + r * S, shard, len);
+        enc->host_round = true;
+        if ((r + 1 - enc->run0) * S >= STREAM_BYTES) {
+            if (int rc = enc->eng->activate(err)) return rc;
+            if (int rc = encoder_stream(enc, r + 1, err)) return rc;
+        }
+    }
+    enc->received = r + 1;
     return set_error(err, RS16_OK);
 }
 extern "C" int rs16_encoder_add_original_shard(rs16_encoder* enc, const void* shard, size_t len, rs16_error* err) {
@@ -416,12 +490,25 @@ extern "C" int rs16_encoder_add_original_shard(rs16_encoder* enc, const void* sh
 extern "C" int rs16_encoder_add_original_shard_device(rs16_encoder* enc, const void* d, size_t len, rs16_error* err) {
     return encoder_add(enc, d, len, true, err);
 }
+// D2H of every recovery row into h_out (once per round).
+static int encoder_fetch(rs16_encoder* enc, rs16_error* err) {
+    if (enc->out_on_host) return RS16_OK;
+    RS16_HIP(enc->h_out.reserve(enc->m * enc->S));
+    RS16_HIP(hipMemcpyAsync(enc->h_out.p, enc->work.p, enc->m * enc->S, hipMemcpyDeviceToHost, enc->eng->stream));
+    RS16_HIP(enc->out_done.record(enc->eng->stream));
+    enc->out_on_host = true;
+    return RS16_OK;
+}
 extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
     if (!enc->eng || enc->encoded) return set_error(err, RS16_INVALID_ARGUMENT);
     if (enc->received != enc->k) return set_error(err, RS16_TOO_FEW_ORIGINAL_SHARDS, enc->k, enc->received);
     rs16_engine* e = enc->eng;
     if (int rc = e->activate(err)) return rc;
     if (int rc = e->order(e->stream, err)) return rc;
+    if (enc->host_round) {
+        if (int rc = encoder_stream(enc, enc->received, err)) return rc;
+        RS16_HIP(enc->in_done.record(e->stream));
+    }
     uint8_t* w = (uint8_t*)enc->work.p;
     const size_t chunk = next_pow2(enc->m);
     int rc;
@@ -432,26 +519,36 @@ extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
     else
         rc = e->encode_low_generic(enc->k, enc->m, enc->S, w, enc->work_count, e->stream, err);
     if (rc) return rc;
+    if (int rc2 = e->scratch_done(e->stream, err)) return rc2;
+    // a host round gets its results back in one copy, right behind the passes
+    if (enc->host_round)
+        if (int rc2 = encoder_fetch(enc, err)) return rc2;
     enc->encoded = true;
     return set_error(err, RS16_OK);
 }
 extern "C" const void* rs16_encoder_recovery_device(rs16_encoder* enc, size_t index) {
     return enc->eng && enc->encoded && index < enc->m ? (const uint8_t*)enc->work.p + index * enc->S : nullptr;
 }
+static const void* encoder_recovery_host(rs16_encoder* enc, size_t index, rs16_error* err) {
+    if (!(enc->eng && enc->encoded && index < enc->m)) return set_error(err, RS16_OK), nullptr;
+    if (enc->eng->activate(err) || encoder_fetch(enc, err)) return nullptr;
+    hipError_t he = enc->out_done.wait();
+    if (he != hipSuccess) return hip_fail(err, he), nullptr;
+    set_error(err, RS16_OK);
+    return (const uint8_t*)enc->h_out.p + index * enc->S;
+}
+extern "C" const void* rs16_encoder_recovery(rs16_encoder* enc, size_t index, rs16_error* err) {
+    return encoder_recovery_host(enc, index, err);
+}
 extern "C" int rs16_encoder_recovery_copy(rs16_encoder* enc, size_t index, void* dst, size_t len, rs16_error* err) {
-    const void* src = rs16_encoder_recovery_device(enc, index);
-    if (!src) return set_error(err, RS16_OK), 0;
+    if (!rs16_encoder_recovery_device(enc, index)) return set_error(err, RS16_OK), 0;
     if (len < enc->S) return set_error(err, RS16_INVALID_ARGUMENT), -1;
-    if (enc->eng->activate(err)) return -1;  // (src != nullptr: attached)
-    hipError_t he = hipMemcpyAsync(dst, src, enc->S, hipMemcpyDeviceToHost, enc->eng->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(enc->eng->stream);
-    if (he != hipSuccess) return hip_fail(err, he), -1;
-    return set_error(err, RS16_OK), 1;
+    const void* src = encoder_recovery_host(enc, index, err);
+    if (!src) return -1;
+    memcpy(dst, src, enc->S);
+    return 1;
 }
-extern "C" void rs16_encoder_result_drop(rs16_encoder* enc) {
-    enc->received = 0;
-    enc->encoded = false;
-}
+extern "C" void rs16_encoder_result_drop(rs16_encoder* enc) { encoder_new_round(enc); }
 extern "C" int rs16_encoder_is_high_rate(const rs16_encoder* enc) { return enc->high; }
 
 // ---------------------------------------------------------------------------
@@ -469,13 +566,37 @@ struct rs16_decoder {
     size_t orig_base = 0, rec_base = 0, orig_recv = 0, rec_recv = 0;
     std::vector<uint8_t> received;  // by work position
     DevBuf work, ubuf, flags;       // work = shards (z), ubuf = second work array (u)
+    // Host staging: h_img is a page-locked image of the work layout.  hrow[pos]
+    // = 1: row pos was added from host memory and is not yet on the device;
+    // [run_lo, run_hi) is the latest stretch of consecutive host rows (it
+    // streams to HBM once it reaches STREAM_BYTES).  h_flags: the received
+    // flags of the two segments, for the device.
+    HostBuf h_img, h_flags, h_out;  // h_out: restored originals, row = original index
+    std::vector<uint8_t> hrow;
+    size_t run_lo = 0, run_hi = 0;
+    bool host_round = false, dev_round = false, out_on_host = false;
+    Pending in_done, out_done;
 };
 
 static void detach(rs16_decoder* d) {
     d->work.release();
     d->ubuf.release();
     d->flags.release();
+    d->h_img.release();
+    d->h_flags.release();
+    d->h_out.release();
+    d->in_done.release();
+    d->out_done.release();
     d->eng = nullptr;
+}
+
+static void decoder_new_round(rs16_decoder* d) {
+    d->decoded = false;
+    d->orig_recv = d->rec_recv = 0;
+    std::fill(d->received.begin(), d->received.end(), 0);
+    std::fill(d->hrow.begin(), d->hrow.end(), 0);
+    d->run_lo = d->run_hi = 0;
+    d->host_round = d->dev_round = d->out_on_host = false;
 }
 
 static int decoder_reset_impl(rs16_decoder* d, size_t k, size_t m, size_t S, rs16_error* err) {
@@ -494,9 +615,9 @@ static int decoder_reset_impl(rs16_decoder* d, size_t k, size_t m, size_t S, rs1
     d->work_count = wc;
     d->orig_base = high ? next_pow2(m) : 0;  // rate_high.rs:279-299 / rate_low.rs:279-299
     d->rec_base = high ? 0 : next_pow2(k);
-    d->orig_recv = d->rec_recv = 0;
-    d->decoded = false;
     d->received.assign(std::max(d->received.size(), wc), 0);
+    d->hrow.assign(std::max(d->hrow.size(), wc), 0);
+    decoder_new_round(d);
     return set_error(err, RS16_OK);
 }
 
@@ -526,6 +647,37 @@ extern "C" void rs16_decoder_free(rs16_decoder* d) {
 extern "C" int rs16_decoder_reset(rs16_decoder* d, size_t k, size_t m, size_t S, rs16_error* err) {
     return decoder_reset_impl(d, k, m, S, err);
 }
+// Copy host rows [lo, hi) of the image to the device work rows.
+static int decoder_stream(rs16_decoder* d, size_t lo, size_t hi, rs16_error* err) {
+    const size_t S = d->S;
+    RS16_HIP(hipMemcpyAsync((uint8_t*)d->work.p + lo * S, (const uint8_t*)d->h_img.p + lo * S, (hi - lo) * S,
+                            hipMemcpyHostToDevice, d->eng->stream));
+    std::fill(d->hrow.begin() + lo, d->hrow.begin() + hi, 0);
+    return RS16_OK;
+}
+// Every host row not yet on the device: maximal runs of such rows, or one
+// copy of their whole span when they are scattered (rows in between were
+// not received, and their device contents are never read -- unless a row
+// in between came from device memory: then run by run).
+static int decoder_stream_all(rs16_decoder* d, rs16_error* err) {
+    const size_t wc = d->work_count;
+    std::vector<std::pair<size_t, size_t>> runs;
+    for (size_t i = 0; i < wc;) {
+        if (!d->hrow[i]) {
+            i++;
+            continue;
+        }
+        size_t j = i;
+        while (j < wc && d->hrow[j]) j++;
+        runs.push_back({i, j});
+        i = j;
+    }
+    if (runs.empty()) return RS16_OK;
+    if (runs.size() > 32 && !d->dev_round) return decoder_stream(d, runs.front().first, runs.back().second, err);
+    for (auto& r : runs)
+        if (int rc = decoder_stream(d, r.first, r.second, err)) return rc;
+    return RS16_OK;
+}
 static int decoder_add(rs16_decoder* d, bool original, size_t index, const void* shard, size_t len, bool device,
                        rs16_error* err) {
     if (!d->eng || d->decoded) return set_error(err, RS16_INVALID_ARGUMENT);
@@ -538,10 +690,28 @@ static int decoder_add(rs16_decoder* d, bool original, size_t index, const void*
         return set_error(err, original ? RS16_DUPLICATE_ORIGINAL_SHARD_INDEX : RS16_DUPLICATE_RECOVERY_SHARD_INDEX,
                          index);
     if (len != d->S) return set_error(err, RS16_DIFFERENT_SHARD_SIZE, d->S, len);
-    if (int rc = d->eng->activate(err)) return rc;
-    uint8_t* dst = (uint8_t*)d->work.p + pos * d->S;
-    RS16_HIP(hipMemcpyAsync(dst, shard, len, device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, d->eng->stream));
-    if (!device) RS16_HIP(hipStreamSynchronize(d->eng->stream));
+    const size_t S = d->S;
+    if (device) {
+        if (int rc = d->eng->activate(err)) return rc;
+        RS16_HIP(hipMemcpyAsync((uint8_t*)d->work.p + pos * S, shard, len, hipMemcpyDeviceToDevice, d->eng->stream));
+        d->dev_round = true;
+    } else {
+        if (!d->host_round) {
+            // the previous round's copies out of the image must be done
+            RS16_HIP(d->in_done.wait());
+            RS16_HIP(d->h_img.reserve(d->work_count * S));
+            d->host_round = true;
+        }
+        memcpy((uint8_t*)d->h_img.p + pos * S, shard, len);
+        d->hrow[pos] = 1;
+        if (pos == d->run_hi && d->run_hi > d->run_lo) d->run_hi++;
+        else d->run_lo = pos, d->run_hi = pos + 1;
+        if ((d->run_hi - d->run_lo) * S >= STREAM_BYTES) {
+            if (int rc = d->eng->activate(err)) return rc;
+            if (int rc = decoder_stream(d, d->run_lo, d->run_hi, err)) return rc;
+            d->run_lo = d->run_hi;
+        }
+    }
     (original ? d->orig_recv : d->rec_recv)++;
     d->received[pos] = 1;
     return set_error(err, RS16_OK);
@@ -560,6 +730,23 @@ extern "C" int rs16_decoder_add_recovery_shard_device(rs16_decoder* d, size_t i,
                                                       rs16_error* err) {
     return decoder_add(d, false, i, s, len, true, err);
 }
+// D2H of the lost originals' rows into h_out (one copy of their span;
+// received rows inside it come back as scratch, and are never read there).
+static int decoder_fetch(rs16_decoder* d, rs16_error* err) {
+    if (d->out_on_host) return RS16_OK;
+    size_t lo = d->k, hi = 0;
+    for (size_t i = 0; i < d->k; i++)
+        if (!d->received[d->orig_base + i]) lo = std::min(lo, i), hi = i + 1;
+    if (hi > lo) {
+        const size_t S = d->S;
+        RS16_HIP(d->h_out.reserve(d->k * S));
+        RS16_HIP(hipMemcpyAsync((uint8_t*)d->h_out.p + lo * S, (const uint8_t*)d->work.p + (d->orig_base + lo) * S,
+                                (hi - lo) * S, hipMemcpyDeviceToHost, d->eng->stream));
+        RS16_HIP(d->out_done.record(d->eng->stream));
+    }
+    d->out_on_host = true;
+    return RS16_OK;
+}
 extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
     if (!d->eng || d->decoded) return set_error(err, RS16_INVALID_ARGUMENT);
     // decode_begin (src/rate/decoder_work.rs:120-139)
@@ -569,18 +756,29 @@ extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
     rs16_engine* e = d->eng;
     if (int rc = e->activate(err)) return rc;
     if (int rc = e->order(e->stream, err)) return rc;
+    if (int rc = decoder_stream_all(d, err)) return rc;
     DecodeGeom g = decode_geom(d->high, d->k, d->m);
     g.a_recv = d->high ? d->rec_recv : d->orig_recv;
     g.b_recv = d->high ? d->orig_recv : d->rec_recv;
-    // Received flags of the two segments -> device (bytes, one per row).
+    // Received flags of the two segments -> device (bytes, one per row), out
+    // of the page-locked staging (written once the previous round's copies
+    // out of it are done).
+    if (!d->host_round) RS16_HIP(d->in_done.wait());
+    RS16_HIP(d->h_flags.reserve(GF_ORDER * 2));
+    uint8_t* hf = (uint8_t*)d->h_flags.p;
+    memcpy(hf, d->received.data(), g.a_count);
+    memcpy(hf + GF_ORDER, d->received.data() + g.chunk, g.b_count);
     uint8_t* fl = (uint8_t*)d->flags.p;
-    RS16_HIP(hipMemcpyAsync(fl, d->received.data(), g.a_count, hipMemcpyHostToDevice, e->stream));
-    RS16_HIP(hipMemcpyAsync(fl + GF_ORDER, d->received.data() + g.chunk, g.b_count, hipMemcpyHostToDevice, e->stream));
+    RS16_HIP(hipMemcpyAsync(fl, hf, g.a_count, hipMemcpyHostToDevice, e->stream));
+    RS16_HIP(hipMemcpyAsync(fl + GF_ORDER, hf + GF_ORDER, g.b_count, hipMemcpyHostToDevice, e->stream));
+    RS16_HIP(d->in_done.record(e->stream));
     uint8_t* w = (uint8_t*)d->work.p;
     if (int rc = e->decode_fused(g, d->S, d->S, w, fl, w + (size_t)g.chunk * d->S, fl + GF_ORDER, w + d->orig_base * d->S,
                                  w, (uint8_t*)d->ubuf.p, e->stream, err))
         return rc;
-    RS16_HIP(hipStreamSynchronize(e->stream));  // host flag buffers are pageable
+    if (int rc = e->scratch_done(e->stream, err)) return rc;
+    if (d->host_round)
+        if (int rc = decoder_fetch(d, err)) return rc;
     d->decoded = true;
     return set_error(err, RS16_OK);
 }
@@ -589,21 +787,28 @@ extern "C" const void* rs16_decoder_restored_original_device(rs16_decoder* d, si
     if (d->eng && d->decoded && index < d->k && !d->received[pos]) return (const uint8_t*)d->work.p + pos * d->S;
     return nullptr;
 }
+static const void* decoder_restored_host(rs16_decoder* d, size_t index, rs16_error* err) {
+    if (!rs16_decoder_restored_original_device(d, index)) return set_error(err, RS16_OK), nullptr;
+    if (d->eng->activate(err) || decoder_fetch(d, err)) return nullptr;
+    hipError_t he = d->out_done.wait();
+    if (he != hipSuccess) return hip_fail(err, he), nullptr;
+    set_error(err, RS16_OK);
+    return (const uint8_t*)d->h_out.p + index * d->S;
+}
+extern "C" const void* rs16_decoder_restored_original(rs16_decoder* d, size_t index, rs16_error* err) {
+    return decoder_restored_host(d, index, err);
+}
 extern "C" int rs16_decoder_restored_original_copy(rs16_decoder* d, size_t index, void* dst, size_t len,
                                                    rs16_error* err) {
-    const void* src = rs16_decoder_restored_original_device(d, index);
-    if (!src) return set_error(err, RS16_OK), 0;
+    if (!rs16_decoder_restored_original_device(d, index)) return set_error(err, RS16_OK), 0;
     if (len < d->S) return set_error(err, RS16_INVALID_ARGUMENT), -1;
-    if (d->eng->activate(err)) return -1;
-    hipError_t he = hipMemcpyAsync(dst, src, d->S, hipMemcpyDeviceToHost, d->eng->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(d->eng->stream);
-    if (he != hipSuccess) return hip_fail(err, he), -1;
-    return set_error(err, RS16_OK), 1;
+    const void* src = decoder_restored_host(d, index, err);
+    if (!src) return -1;
+    memcpy(dst, src, d->S);
+    return 1;
 }
 extern "C" void rs16_decoder_result_drop(rs16_decoder* d) {  // DecoderWork::reset_received
-    d->decoded = false;
-    d->orig_recv = d->rec_recv = 0;
-    std::fill(d->received.begin(), d->received.end(), 0);
+    decoder_new_round(d);
 }
 extern "C" int rs16_decoder_is_high_rate(const rs16_decoder* d) { return d->high; }
 
@@ -637,6 +842,7 @@ extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
         if (int rc = encode_dev(e, high, k, m, S, (const uint8_t*)d_original, (uint8_t*)d_recovery,
                                 (uint8_t*)e->ws_z.p, s, err))
             return rc;
+        if (int rc = e->scratch_done(s, err)) return rc;
         return set_error(err, RS16_OK);
     }
     // column slices on the engine's slice streams (work space: wc x width each)
@@ -650,6 +856,7 @@ extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
         b0 = (int)b1;
     }
     if (int rc = e->join(s, n, err)) return rc;
+    if (int rc = e->scratch_done(s, err)) return rc;
     return set_error(err, RS16_OK);
 }
 
@@ -701,6 +908,7 @@ extern "C" int rs16_encode_host(rs16_engine* e, size_t k, size_t m, size_t S, co
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_recovery + off, S, sl.rec.p, w, w, m, hipMemcpyDeviceToHost, sl.s));
     }
     for (auto& sl : e->hslot) RS16_HIP(hipStreamSynchronize(sl.s));
+    if (int rc = e->scratch_done(e->stream, err)) return rc;
     return set_error(err, RS16_OK);
 }
 
@@ -754,6 +962,7 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_original + off, S, sl.orig.p, w, w, k, hipMemcpyDeviceToHost, sl.s));
     }
     for (auto& sl : e->hslot) RS16_HIP(hipStreamSynchronize(sl.s));
+    if (int rc = e->scratch_done(e->stream, err)) return rc;
     return set_error(err, RS16_OK);
 }
 
@@ -787,6 +996,7 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
         if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
                                       (uint8_t*)e->ws_u.p, s, err))
             return rc;
+        if (int rc = e->scratch_done(s, err)) return rc;
         return set_error(err, RS16_OK);
     }
     if (int rc = e->fork(s, n, err)) return rc;
@@ -800,6 +1010,7 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
         b0 = (int)b1;
     }
     if (int rc = e->join(s, n, err)) return rc;
+    if (int rc = e->scratch_done(s, err)) return rc;
     return set_error(err, RS16_OK);
 }
 
@@ -831,7 +1042,6 @@ extern "C" void rs16_stream_destroy(rs16_engine* e, void* st) {
     if (!e || !st) return;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize((hipStream_t)st);
-    if (e->last_stream == (hipStream_t)st) e->last_stream = nullptr;
     (void)hipStreamDestroy((hipStream_t)st);
 }
 extern "C" void* rs16_host_alloc(rs16_engine* e, size_t bytes, rs16_error* err) {

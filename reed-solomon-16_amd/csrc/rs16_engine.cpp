@@ -8,6 +8,8 @@
 
 namespace rs16 {
 
+int g_diag = 0;
+
 hipError_t DevBuf::reserve(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipFree(p);
@@ -21,6 +23,41 @@ void DevBuf::release() {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
+}
+
+hipError_t HostBuf::reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+}
+void HostBuf::release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+hipError_t Pending::record(hipStream_t s) {
+    if (!ev) {
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipEventRecord(ev, s);
+    busy = e == hipSuccess;
+    return e;
+}
+hipError_t Pending::wait() {
+    if (!busy) return hipSuccess;
+    busy = false;
+    return hipEventSynchronize(ev);
+}
+void Pending::release() {
+    if (ev) (void)hipEventDestroy(ev);
+    ev = nullptr;
+    busy = false;
 }
 
 int set_error(rs16_error* err, int code, uint64_t v0, uint64_t v1, uint64_t v2) {
@@ -72,11 +109,7 @@ int rs16_engine::activate(rs16_error* err) {
 }
 
 int rs16_engine::slice_count(size_t S) const {
-    static const int env = [] {
-        const char* v = std::getenv("RS16_SLICES");
-        return v ? std::atoi(v) : 0;
-    }();
-    const int n = env > 0 ? env : slices;
+    const int n = slices;
     return (int)std::max<size_t>(1, std::min<size_t>(std::min(n, MAX_SLICES), S / 64));
 }
 
@@ -104,12 +137,24 @@ int rs16_engine::join(hipStream_t s, int n, rs16_error* err) {
 }
 
 int rs16_engine::order(hipStream_t s, rs16_error* err) {
-    if (last_stream && last_stream != s) {
+    if (last == LAST_ENGINE && s != stream) {
         if (!order_ev) RS16_HIP(hipEventCreateWithFlags(&order_ev, hipEventDisableTiming));
-        RS16_HIP(hipEventRecord(order_ev, last_stream));
+        RS16_HIP(hipEventRecord(order_ev, stream));
         RS16_HIP(hipStreamWaitEvent(s, order_ev, 0));
+    } else if (last == LAST_CALLER) {
+        RS16_HIP(hipStreamWaitEvent(s, order_ev, 0));  // (recorded by scratch_done)
     }
-    last_stream = s;
+    return RS16_OK;
+}
+
+int rs16_engine::scratch_done(hipStream_t s, rs16_error* err) {
+    if (s == stream) {
+        last = LAST_ENGINE;
+        return RS16_OK;
+    }
+    if (!order_ev) RS16_HIP(hipEventCreateWithFlags(&order_ev, hipEventDisableTiming));
+    RS16_HIP(hipEventRecord(order_ev, s));
+    last = LAST_CALLER;
     return RS16_OK;
 }
 
@@ -231,12 +276,9 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
         RS16_PASS(ENC_SINGLE, L, a, 1, s);
         return RS16_OK;
     }
-#ifndef RS16_ENC_LO_UP
-#define RS16_ENC_LO_UP 0
-#endif
-    // odd L: the extra row bit goes to the strided two-direction pass (0) or
-    // to the contiguous first / last passes (1)
-    const int lo = (L + RS16_ENC_LO_UP) / 2, hi = L - lo;
+    // odd L: the extra row bit goes to the strided two-direction pass (an
+    // 8 / 7 / 8 split measured 2-3 us slower per encode)
+    const int lo = L / 2, hi = L - lo;
     a.out = Z;
     a.lo = 0;
     RS16_PASS(ENC_FIRST, lo, a, 1u << hi, s);
@@ -266,15 +308,6 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, size_t S_user, cons
                               hipStream_t s, rs16_error* err) {
     if (int rc = decode_eval(g, flags_a, flags_b, s, err)) return rc;
     return decode_passes(g, S, S_user, seg_a, flags_a, seg_b, flags_b, rest, Z, U, s, err);
-}
-
-// RS16_EVAL_FULL=1 (diagnostic): always the 3-kernel 65536-point eval_poly.
-static bool eval_full_forced() {
-    static const bool f = [] {
-        const char* v = std::getenv("RS16_EVAL_FULL");
-        return v && v[0] == '1';
-    }();
-    return f;
 }
 
 // Erasure logs e = eval_poly(erasure vector) into ws_elog (2-3 small kernels).
@@ -313,7 +346,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // 256-point FWHT themselves, for the 256-row block of their tile's rows
     // (one kernel less) -- except the one-pass half-transform decode, whose
     // gather and reveal rows lie in different blocks.
-    const bool small = g.high && g.n <= 2048 && !eval_full_forced();
+    const bool small = g.high && g.n <= 2048 && !(g_diag & DIAG_EVAL_FULL);
     elog_fused = !(half_decode(g) && ilog2(g.n) - 1 <= 8);
     if (small) {
         // erasures are zero from row n on: only n/256 live blocks (rs16_misc.hip)

@@ -16,6 +16,21 @@ struct DevBuf {
     hipError_t reserve(size_t bytes);
     void release();
 };
+// Grow-only page-locked host buffer (hipHostMalloc): DMA-rate H2D / D2H.
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes);
+    void release();
+};
+// An event recorded on a stream and not yet waited for on the host.
+struct Pending {
+    hipEvent_t ev = nullptr;
+    bool busy = false;
+    hipError_t record(hipStream_t s);
+    hipError_t wait();  // host-side: returns once the recorded work is done
+    void release();
+};
 
 // Status helper: every internal call returns an rs16 code and fills err.
 int set_error(rs16_error* err, int code, uint64_t v0 = 0, uint64_t v1 = 0, uint64_t v2 = 0);
@@ -101,11 +116,18 @@ struct rs16_engine {
 
     // The scratch buffers (ws_*) belong to the engine, not to a stream: a
     // call that uses them on stream s first waits for the engine's previous
-    // such call when that ran on another stream (one event, recorded there),
-    // so calls on different streams cannot overwrite each other's scratch.
-    hipStream_t last_stream = nullptr;
+    // such call when that ran on another stream, so calls on different
+    // streams cannot overwrite each other's scratch.  order(s) at the start
+    // of such a call, scratch_done(s) at its end.  A call on a caller's
+    // stream records order_ev there before it returns (the stream is never
+    // touched again: the caller may destroy it); a call on the engine's own
+    // stream records nothing unless a later call on another stream needs it
+    // (then it is recorded on the engine stream, which the engine owns), so
+    // the one-stream case costs no event.
+    enum { LAST_NONE, LAST_ENGINE, LAST_CALLER } last = LAST_NONE;
     hipEvent_t order_ev = nullptr;
     int order(hipStream_t s, rs16_error* err);
+    int scratch_done(hipStream_t s, rs16_error* err);
 
     // Encoders / decoders created on this engine.  rs16_engine_free releases
     // their device work space and detaches them (eng = nullptr): a detached

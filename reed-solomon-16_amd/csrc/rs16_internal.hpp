@@ -67,11 +67,9 @@ struct PassArgs {
     uint64_t S_in, S_out, S_seg, S_rest;
     uint32_t qrow;             // quads per row of the slice = width / 8
     uint32_t nslab;            // ceil(qrow / Q), set by launch_pass
-    // Persistent pass: the launch covers ntiles tiles x nslab slabs = items,
-    // item i = (tile i / nslab, slab i % nslab); workgroup b processes items
-    // [b * per_wg, (b + 1) * per_wg) in order, loading item i + 1 while it
-    // computes item i.  Set by launch_pass.
-    uint32_t ntiles, per_wg;
+    // The launch covers ntiles tiles x nslab slabs = items, one workgroup
+    // per item (set_item maps workgroups to items XCD-aware).  Set by launch_pass.
+    uint32_t ntiles;
     uint32_t lo;               // tile bit offset
     uint32_t a_count, chunk, b_count;
     uint32_t skew_ifft, skew_fft;
@@ -121,6 +119,16 @@ struct PassArgs {
     // diagnostic timeline buffer (RS16_STAMPS builds; nullptr otherwise)
     uint64_t* stamps;
 };
+
+// Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):
+// alternative code paths kept for tests and measurements, never needed for
+// correct results.  0 = the shipped behaviour.
+enum DiagFlags : int {
+    DIAG_FORCE_VOFF64 = 1,    // 64-bit lane offsets in every pass (PassArgs::voff32 = 0)
+    DIAG_EVAL_TWO_KERNEL = 2, // eval_poly: two-kernel form even when the one-kernel form applies
+    DIAG_EVAL_FULL = 4,       // eval_poly: the full 65536-point form even for n <= 2048
+};
+extern int g_diag;
 
 constexpr size_t RS16_ZERO_BYTES = 65536;
 constexpr size_t RS16_SINK_BYTES = 1 << 20;

@@ -444,11 +444,7 @@ static bool eval_fused_ok(const ErasureSpec& e) {
 
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
-    static const int mode = [] {  // RS16_EVAL_FUSED=0: always the two-kernel form
-        const char* v = std::getenv("RS16_EVAL_FUSED");
-        return v ? std::atoi(v) : 1;
-    }();
-    if (mode && eval_fused_ok(e)) {
+    if (!(g_diag & DIAG_EVAL_TWO_KERNEL) && eval_fused_ok(e)) {
         hipLaunchKernelGGL(eval_fused_kernel, dim3(256), dim3(256), 0, s, e, work, log_walsh);
     } else {
         hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(64), 0, s, e, work);

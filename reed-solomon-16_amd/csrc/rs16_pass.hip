@@ -14,26 +14,21 @@
 //   contiguous tiles, lo > 0 strided ones; the slab of an item selects its Q
 //   quads of the row.
 //
-//   Software pipeline: the grid is persistent (two 4-wave workgroups per CU
-//   for T >= 6).  Workgroup b takes a contiguous run of items and issues the
-//   HBM loads of item i + 1 into a second register set before it computes
-//   item i, so the loads of the next item and the stores of the previous one
-//   run under the butterflies instead of in a load phase and a store phase
-//   of their own (all workgroups of a one-item-per-workgroup grid load, then
-//   compute, then store in step).
+//   One item per workgroup: the twiddle tables of the tile are requested
+//   first and the tile's rows right behind them, then staged, computed and
+//   stored (a software-pipelined persistent variant
+//   measured slower at every T).
 //
 //   Lane = quad.  Each thread keeps 16 rows ("a row set") of its quad in
-//   VGPRs; a wave holds 64/Q row sets (T = 8: Q = 16, 4 row sets; T = 7:
-//   Q = 32; T = 6: Q = 64).  The 4 layers whose row bits are in registers
+//   VGPRs (8 at T = 5); a wave holds 64/Q row sets (Q = 32 quads per tile row
+//   from T = 5 on: 2 row sets per wave).  The 4 layers whose row bits are in registers
 //   are radix-16 butterfly networks with no data movement; an LDS transpose
 //   switches between layout A (k bits 0-3 in registers) and layout B (k bits
 //   T-4..T-1).
 //
 //   Twiddle tables: a tile needs 2^T - 1 distinct twiddles per transform
 //   direction (one per (layer, group)).  Their 80-byte v_perm multiply tables
-//   are staged into LDS when a workgroup starts a new tile key (b_high: the
-//   twiddles of a strided pass are the same for every tile of a transform,
-//   so they are staged once per workgroup) and read with ds_read_b128
+//   are staged into LDS (one level of loads from skew_tab) and read with ds_read_b128
 //   (5 per group, broadcast within each row set), one group ahead of use.
 //   Groups are compiled as a straight-line sequence separated by register
 //   pins, so a wave holds at most two tables.  The decoder's per-row erasure
@@ -52,8 +47,6 @@
 //   DEC_MID to read those rows as zero and to skip the IFFT groups whose rows
 //   all are, and DEC_LAST that its z term is zero (y = u + L(z) = u).  At
 //   100 % original loss this is the whole original half of the decode work.
-#include <cstdlib>
-
 #include "rs16_internal.hpp"
 
 namespace rs16 {
@@ -63,15 +56,9 @@ typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 enum LoadMode { LD_PLAIN = 0, LD_GATHER_ENC, LD_GATHER_DEC, LD_DEC_LAST };
 enum StoreMode { ST_PLAIN = 0, ST_RECOVERY, ST_RESTORE };
 
-// Store cache policy (RS16_STPOL): 0 plain, 1 nt on the single-direction
-// passes, 4 nt everywhere, 2 sc1 (agent scope: the line leaves the XCD's L2
-// at once), 3 sc0 sc1 (system scope).  Load policy (RS16_LDPOL): 0 plain, 1 nt.
-#ifndef RS16_STPOL
-#define RS16_STPOL 1
-#endif
-#ifndef RS16_LDPOL
-#define RS16_LDPOL 0
-#endif
+// Store cache policy: non-temporal stores in the single-direction passes,
+// plain stores in the two-direction passes (same-box A/B, DESIGN.md 6.1:
+// nt / sc1 / sc0 sc1 everywhere and nt loads all measured slower).
 template <int P> struct ProgTraits;
 #define RS16_PROG(P, LD, I, F, FF, ST)          \
     template <> struct ProgTraits<P> {         \
@@ -80,8 +67,7 @@ template <int P> struct ProgTraits;
         static constexpr bool FD = F;          \
         static constexpr bool FFT = FF;        \
         static constexpr int STORE = ST;       \
-        static constexpr bool ST_NT = RS16_STPOL == 4 || (RS16_STPOL == 1 && !(I && FF)) || \
-                                      (RS16_STPOL == 5 && ST != ST_PLAIN);                  \
+        static constexpr bool ST_NT = !(I && FF);                                           \
     };
 RS16_PROG(GEN_FFT, LD_PLAIN, false, false, true, ST_PLAIN)
 RS16_PROG(GEN_IFFT, LD_PLAIN, true, false, false, ST_PLAIN)
@@ -97,34 +83,18 @@ RS16_PROG(DEC_HALF_LAST, LD_PLAIN, false, false, true, ST_RESTORE)
 RS16_PROG(DEC_HALF_SINGLE, LD_GATHER_DEC, true, false, true, ST_RESTORE)
 #undef RS16_PROG
 
-// RS16_PIPE = 1: software-pipelined persistent passes (4-wave workgroups,
-// two per CU, the next item's rows prefetched into a second register set);
-// 0: one item per workgroup, no prefetch, 4 waves per SIMD (32 quads per
-// tile row from T = 5 on).
-#ifndef RS16_PIPE
-#define RS16_PIPE 0
-#endif
-// Quads per tile row at T = 8 in the one-item build: 32 (8-wave workgroups,
-// two per CU) or 16 (4-wave workgroups, four per CU).
-#ifndef RS16_Q8
-#define RS16_Q8 32
-#endif
-// Row bits in registers at T = 5 (the passes of the n <= 2048 codecs, which
-// are latency-bound: 128 waves at 16 rows per thread): 3 = 8 rows per thread
-// and 16 quads per tile row, twice the waves, each with half the butterfly
-// chain; 4 = the 16-row geometry of the larger passes.
-#ifndef RS16_R5
-#define RS16_R5 3
-#endif
+// Row bits in registers: 4 (16 rows per thread) from T = 6 on; 3 at T = 5
+// (the passes of the n <= 2048 codecs, which are latency-bound: 8 rows per
+// thread and 16 quads per tile row give twice the waves, each with half the
+// butterfly chain).  At T = 8 a tile row has 32 quads (8-wave workgroups,
+// two per CU; 16 quads in 4-wave workgroups measured slower).
 template <int T> struct Geo {
-    static constexpr int R = T > 4 ? (T == 5 ? RS16_R5 : 4) : T;  // row bits held in registers
+    static constexpr int R = T > 4 ? (T == 5 ? 3 : 4) : T;  // row bits held in registers
     static constexpr int NR = 1 << R;                     // rows per thread (a row set)
     static constexpr int SETS = 1 << (T - R);             // row sets per tile
-    // quads per tile row: PIPE: 4 waves per workgroup from T = 6 on
-    // (Q = 256 / SETS); else 32 (two 16-row sets per wave) from T = 5 on,
-    // 16 (four 8-row sets per wave) at T = 5 with 8 rows per thread
-    static constexpr int Q = (RS16_PIPE && T >= 6) ? 256 / SETS
-                                                   : (T == 8 ? RS16_Q8 : (T > 4 ? (R == 3 ? 16 : 32) : 64));
+    // quads per tile row: 32 (two 16-row sets per wave) from T = 6 on, 16
+    // (four 8-row sets per wave) at T = 5, 64 (one row set) below
+    static constexpr int Q = T > 4 ? (R == 3 ? 16 : 32) : 64;
     static constexpr int HWS = 64 / Q;                    // row sets per wave
     static constexpr int W = SETS / HWS > 0 ? SETS / HWS : 1;  // waves per workgroup
     static constexpr int SHB = T - R;                     // layout B: k = s + (m << SHB)
@@ -137,7 +107,7 @@ template <int T> struct Geo {
 // The layout switch goes through the LDS image in one round (32 KiB at
 // T = 6..8: 2^T rows x Q quads x 8 bytes).
 template <int P, int T> struct Rnd {
-    static constexpr int NQR = (!RS16_PIPE && T >= 7) ? 2 : 1;
+    static constexpr int NQR = T >= 7 ? 2 : 1;
     static constexpr int QL = Geo<T>::Q / NQR;
 };
 
@@ -159,7 +129,7 @@ template <int P, int T> struct Smem {
     // Restage (one-item build, T > 4): tab2 holds only the second
     // direction's layout-B tables; its layout-A tables are written over the
     // first direction's in tab1 at the first layout switch.
-    static constexpr bool RESTAGE = TWO && T > 4 && !RS16_PIPE;
+    static constexpr bool RESTAGE = TWO && T > 4;
     static constexpr int TAB2_BYTES = TWO ? (RESTAGE ? Geo<T>::NTAB - Geo<T>::TSPLIT : Geo<T>::NTAB) * 80 : 0;
     static constexpr int RVT_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 80 : 0;
     static constexpr int LOST_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 4 : 0;
@@ -234,9 +204,6 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
 #ifndef RS16_ABLATE
 #define RS16_ABLATE 0
 #endif
-#ifndef RS16_NO_PIN
-#define RS16_NO_PIN 0
-#endif
 
 // Diagnostic timeline build (-DRS16_STAMPS=1, never the shipped library):
 // wave 0 of every workgroup stores s_memtime at phase boundaries to
@@ -250,28 +217,14 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
 // its item progresses, so that waves that are behind win the arbitration.
 // Hardware age order alone lets the oldest workgroup of a CU run ahead and
 // leaves a low-occupancy one-workgroup tail (scripts/stamps.py: 10-16 us
-// spread of workgroup end times).  Measured (bench, 2 runs each): 1 = all
-// passes 620 / 614 GiB/s, 2 = two-direction passes only 611 / 611, 3 = a
-// later schedule 607, 0 = off 595 / 594.
-#ifndef RS16_PRIO
-#define RS16_PRIO 1
-#endif
-// at point `at` of program P's item (0 staged, 1 first layout-A layers done,
-// 2 first direction done, 3 layout-B FFT done, 4 last switch done, 5 stores)
+// spread of workgroup end times).  Measured (bench, 2 runs each): this
+// schedule 620 / 614 GiB/s; on the two-direction passes only 611 / 611; a
+// later schedule 607; none 595 / 594.
+// At point `at` of program P's item (0 staged, 1 first layout-A layers done,
+// 2 first direction done, 3 layout-B FFT done, 4 last switch done, 5 stores).
 template <int P, int at> __device__ __forceinline__ void prio() {
-#if RS16_PRIO
-    constexpr bool two = ProgTraits<P>::IFFT && ProgTraits<P>::FFT;
-    if constexpr (RS16_PRIO == 1) {
-        constexpr int v[6] = {3, 2, -1, 1, -1, 0};
-        if constexpr (v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
-    } else if constexpr (RS16_PRIO == 2) {
-        constexpr int v[6] = {3, 2, -1, 1, -1, 0};
-        if constexpr (two && v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
-    } else {
-        constexpr int v[6] = {3, -1, 2, -1, 1, 0};
-        if constexpr (two && v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
-    }
-#endif
+    constexpr int v[6] = {3, 2, -1, 1, -1, 0};
+    if constexpr (v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
 }
 
 __device__ __forceinline__ void stamp(const PassArgs& a, int i) {
@@ -296,77 +249,7 @@ __device__ __forceinline__ void stamp(const PassArgs& a, int i) {
 // (expcnt and lgkmcnt at their maxima, i.e. not waited for).
 __host__ __device__ constexpr int vmcnt_wait(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
-template <bool NT> __device__ __forceinline__ void st_dword(uint32_t* p, uint32_t v) {
-    if constexpr (NT) {
-        __builtin_nontemporal_store(v, p);
-    } else if constexpr (RS16_STPOL == 2) {
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if constexpr (RS16_STPOL == 3) {
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-        *p = v;
-    }
-}
-__device__ __forceinline__ uint32_t ld_dword(const uint32_t* p) {
-    if constexpr (RS16_LDPOL == 1) return __builtin_nontemporal_load(p);
-    return *p;
-}
-// Quad loads / stores.  In the pipelined build they have no control flow: a
-// row that is not read (ok = false, or a lane past the row end) comes from
-// the zero page, a row that is not written goes to the sink (PassArgs::zero /
-// sink); the one-item build branches around them.
-__device__ __forceinline__ void ld_quad(const PassArgs& a, const uint8_t* row, bool ok, const Thr& c, uint32_t& L,
-                                        uint32_t& H) {
-#if RS16_ABLATE == 2
-    L = (uint32_t)(uintptr_t)row ^ c.offL ^ (ok ? 1u : 0u);
-    H = L * 3u;
-    return;
-#endif
-#if RS16_PIPE
-    const uint32_t* p = (ok && c.active) ? (const uint32_t*)(row + c.offL)
-                                         : (const uint32_t*)(a.zero + (c.offL & 0x7FFFu));
-    L = p[0];
-    H = p[8];
-#else
-    L = H = 0;
-#if RS16_ABLATE == 5
-    row = a.zero + (((uintptr_t)row >> 10) & 15) * 1024;  // L2-resident 16 KiB
-#endif
-    if (ok && c.active) {
-        const uint32_t* p = (const uint32_t*)(row + c.offL);
-        L = ld_dword(p);
-        H = ld_dword(p + 8);
-    }
-#endif
-}
-// A dropped store: in the pipelined build it goes to the sink (2 KiB per
-// workgroup slot, so that workgroups do not all write the same lines); the
-// one-item build, which needs no exact vmcnt across items, branches.
-template <bool NT = false>
-__device__ __forceinline__ void st_quad(const PassArgs& a, uint8_t* row, bool ok, const Thr& c, uint32_t L,
-                                        uint32_t H) {
-#if RS16_ABLATE == 2
-    if ((L ^ H) != 0x9e3779b9u) return;  // keeps the results live, (almost) never stores
-#endif
-#if RS16_PIPE
-    uint32_t* p = (ok && c.active)
-                      ? (uint32_t*)(row + c.offL)
-                      : (uint32_t*)(a.sink + ((blockIdx.x & (RS16_SINK_BYTES / 2048 - 1)) << 11) + (c.offL & 2047u));
-    p[0] = L;
-    p[8] = H;
-#else
-#if RS16_ABLATE == 5
-    row = a.sink + (((uintptr_t)row >> 10) & 255) * 1024;  // L2-resident 256 KiB
-#endif
-    if (ok && c.active) {
-        uint32_t* p = (uint32_t*)(row + c.offL);
-        st_dword<NT>(p, L);
-        st_dword<NT>(p + 8, H);
-    }
-#endif
-}
-
-// The same for a row address that already includes the lane's offset.
+// Row loads / stores at an address that includes the lane's offset.
 __device__ __forceinline__ void ld_ptr(const PassArgs& a, const gbyte* p, bool ok, uint32_t& L, uint32_t& H) {
 #if RS16_ABLATE == 2
     L = (uint32_t)(uintptr_t)p ^ (ok ? 1u : 0u);
@@ -593,13 +476,10 @@ struct NoFin {
 // all 4 register bits: there the groups run depth-first in pre-order (a
 // group, then its two halves), so rows m, m + 1 are final right after their
 // layer-0 group and can be stored there (EarlyStore).
-#ifndef RS16_EARLY_ST
-#define RS16_EARLY_ST 1
-#endif
 template <int T, bool LB, int KB0, int KB1, bool FFT> struct LayerSeq {
     static constexpr int SH = LB ? Geo<T>::SHB : 0;
     static constexpr int NR = Geo<T>::NR;
-    static constexpr bool DF = RS16_EARLY_ST && FFT && !LB && KB0 == 0 && KB1 == Geo<T>::R && NR >= 8;
+    static constexpr bool DF = FFT && !LB && KB0 == 0 && KB1 == Geo<T>::R && NR >= 8;
     // pre-order of the group tree (node (kb, gi), children (kb-1, 2gi) and
     // (kb-1, 2gi+1)), (kb, gi) packed as kb * 16 + gi; radix 16:
     // (3,0) (2,0) (1,0) (0,0) (0,1) (1,1) (0,2) (0,3) (2,1) (1,2) ...
@@ -654,7 +534,7 @@ __device__ __forceinline__ const uint4* group_table(const Thr& c, const uint4* t
     const uint32_t t = off + j;
     // tab2 starts at the first layout-B table when the layout-A ones are
     // restaged into tab1 (Smem::RESTAGE); T <= 4 has no layout B (TSPLIT = 0)
-    constexpr uint32_t base2 = (!RS16_PIPE && T > 4) ? Geo<T>::TSPLIT : 0;
+    constexpr uint32_t base2 = T > 4 ? Geo<T>::TSPLIT : 0;
     return IN_TAB2 ? tab2 + (t - base2) * 5 : tab1 + t * 5;
 }
 
@@ -716,9 +596,7 @@ struct GroupLoop {
                 }
             }
         }
-#if !RS16_NO_PIN
         pin_rows<Geo<T>::NR>(L, H);
-#endif
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (S::DF && kb == 0) fin(L, H, gi << 1);  // rows 2 gi, 2 gi + 1 are final
         if constexpr (more)
@@ -891,7 +769,6 @@ template <int P, int T> struct ItemRegs {
 // Per-item coordinates of this thread: item -> (tile, slab).
 __device__ __forceinline__ void set_item(Thr& c, const PassArgs& a, uint32_t item, uint32_t Q, uint32_t& tile,
                                          uint32_t& slab) {
-#if !RS16_PIPE
     // One item per workgroup, XCD-aware: workgroups are dealt to the 8 XCDs
     // round-robin (XCD = block mod 8, speed only), so with a tile count that
     // is a multiple of 8 all slabs of a tile run on one XCD (they share the
@@ -905,10 +782,6 @@ __device__ __forceinline__ void set_item(Thr& c, const PassArgs& a, uint32_t ite
         tile = item / a.nslab;
         slab = item - tile * a.nslab;
     }
-#else
-    tile = item / a.nslab;
-    slab = item - tile * a.nslab;
-#endif
     tile += a.tile_base;
     c.b_low = tile & ((1u << a.lo) - 1);
     c.b_high = tile >> a.lo;
@@ -1031,57 +904,9 @@ __device__ __forceinline__ void load_item(const PassArgs& a, const Thr& c, uint3
                 if ((zf[4 * j] & zf[4 * j + 1] & zf[4 * j + 2] & zf[4 * j + 3]) == 0x01010101u) d.zmask |= 1u << j;
         }
     }
-#if !RS16_PIPE
     if (a.voff32) load_rows<P, T, true>(a, c, tile, d);
     else load_rows<P, T, false>(a, c, tile, d);
 }
-#else
-    if constexpr (PT::LOAD == LD_PLAIN) {
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a, a.in + (uint64_t)r * a.S_in, !((d.zrow >> m) & 1u), c, d.L[m], d.H[m]);
-        }
-    } else if constexpr (PT::LOAD == LD_GATHER_ENC) {
-        // HighRateEncoder::encode: work[0..k) = originals, rest zero (rate_high.rs:50-54)
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a, a.seg_a + (uint64_t)r * a.S_seg, r < a.a_count, c, d.L[m], d.H[m]);
-        }
-    } else if constexpr (PT::LOAD == LD_GATHER_DEC) {
-        // received rows (multiplied by their erasure logs in process_item), else
-        // zero.  Received bits of the wave's rows: rows [row0, row0 + 16 HWS)
-        // of the bitmap (row0 a multiple of 16, of 32 when HWS > 1), scalar loads.
-        static_assert(START_B == false && T <= 8, "gather runs in layout A");
-        const uint32_t row0 = row_rel<T>(c, a, (c.w * G::HWS) << R) + a.row_base_in;
-        const cu32p rb = (cu32p)a.rbits + (row0 >> 5);
-        const uint32_t sub = c.s - c.w * G::HWS;
-        uint32_t bits;
-        // (uni(): each word stays a scalar load; a select of two loads would
-        // be folded into one per-lane vector load)
-        if constexpr (G::HWS == 4) bits = ((sub >> 1) ? uni(rb[1]) : uni(rb[0])) >> ((sub & 1) * 16);
-        else if constexpr (G::HWS == 2) bits = uni(rb[0]) >> (sub * 16);
-        else bits = uni(rb[0]) >> (row0 & 31);
-        bits &= (1u << NR) - 1;
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m)) + a.row_base_in;
-            const bool in_b = r >= a.chunk;
-            const uint8_t* src = in_b ? a.seg_b + (uint64_t)(r - a.chunk) * a.S_seg : a.seg_a + (uint64_t)r * a.S_seg;
-            ld_quad(a, src, (bits >> m) & 1u, c, d.L[m], d.H[m]);
-        }
-    } else {  // LD_DEC_LAST: u in registers, z for y = u + L(z)
-        d.ztile = a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u);
-#pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const uint32_t r = row_rel<T>(c, a, kidx<T, START_B>(c, m));
-            ld_quad(a, a.in + (uint64_t)r * a.S_in, !d.ztile, c, d.zl[m], d.zh[m]);
-            ld_quad(a, a.in2 + (uint64_t)r * a.S_in, true, c, d.L[m], d.H[m]);
-        }
-    }
-}
-#endif
 
 // Stage everything that depends on the tile key of the thread's current
 // item: twiddle tables of both directions, and for the decoder's first /
@@ -1216,13 +1041,6 @@ template <int P, int T> struct TileStage {
         __syncthreads();  // staged tables visible
     }
 };
-template <int P, int T>
-__device__ __forceinline__ void stage_tile(const PassArgs& a, const Thr& c, uint32_t tile, uint8_t* smem) {
-    (void)tile;
-    TileStage<P, T> st;
-    st.issue(a, c);
-    st.finish(a, c, smem);
-}
 
 // Compute and store one item whose rows are in d (every thread of the
 // workgroup calls it for the same item).
@@ -1300,7 +1118,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     constexpr bool ZERO_SKIP = P == DEC_MID && T > 4 && G::R == 4;
     // stores inside the last FFT block (one-item build, 16 rows per lane, not
     // the output-pruned DEC_MID; the reveal stores measured slower inside it)
-    constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && !RS16_PIPE && P != DEC_MID && PT::STORE != ST_RESTORE &&
+    constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && P != DEC_MID && PT::STORE != ST_RESTORE &&
                            (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6) && PT::FFT && T > 4;
     uint2* lds = (uint2*)smem;
     const uint4* tab1 = (const uint4*)(smem + SM::TAB1_OFF);
@@ -1427,28 +1245,8 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     cs.b_high = uni(cs.b_high);
     asm volatile("" : "+s"(cs.b_low), "+s"(cs.b_high));
     asm volatile("" : "+v"(cs.offL));
-#if !RS16_PIPE
     if (a.voff32) store_rows<P, T, true>(a, cs, L, H, rvt, lostf);
     else store_rows<P, T, false>(a, cs, L, H, rvt, lostf);
-#else
-#pragma unroll
-    for (int m = 0; m < NR; m++) {
-        const uint32_t k = kidx<T, END_B>(c, m);
-        const uint32_t r = row_rel<T>(cs, a, k);
-        if constexpr (PT::STORE == ST_PLAIN) {
-            st_quad<ProgTraits<P>::ST_NT>(a, a.out + (uint64_t)r * a.S_out, P != DEC_MID || (k >= a.need_lo && k < a.need_hi), cs, L[m], H[m]);
-        } else if constexpr (PT::STORE == ST_RECOVERY) {
-            st_quad<ProgTraits<P>::ST_NT>(a, a.out + (uint64_t)r * a.S_out, r < a.out_rows, cs, L[m], H[m]);
-        } else {
-            uint32_t tt[20];
-            load_table_lds(tt, rvt + k * 5);
-            uint32_t ol = 0, oh = 0;
-            mul_xor(ol, oh, L[m], H[m], tt);
-            const uint32_t i = r + a.row_base_out - (a.rest_seg_b ? a.chunk : 0);
-            st_quad<ProgTraits<P>::ST_NT>(a, a.rest + (uint64_t)i * a.S_rest, lostf[k] != 0, cs, ol, oh);
-        }
-    }
-#endif
     stamp(a, 10);
 #if RS16_STAMPS
     __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
@@ -1456,24 +1254,14 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
 #endif
 }
 
-// The persistent pass: workgroup b processes items [b * per_wg, ...) of the
-// launch, loading item i + 1 while it computes item i.
+// The pass: workgroup b processes item b of the launch (4 waves per SIMD,
+// except the one-pass decoders, whose larger register sets take 1).
 template <int P, int T>
-#ifndef RS16_LDPRIO
-#define RS16_LDPRIO 1
-#endif
-#ifndef RS16_MINW
-#define RS16_MINW (RS16_PIPE ? 2 : 4)
-#endif
-__global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC_HALF_SINGLE) ? 1 : RS16_MINW))
+__global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC_HALF_SINGLE) ? 1 : 4))
     pass_kernel(PassArgs a) {
     using G = Geo<T>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-
-    const uint32_t nitems = a.ntiles * a.nslab;
-    const uint32_t it0 = blockIdx.x * a.per_wg;
-    const uint32_t it1 = min(it0 + a.per_wg, nitems);
-    if (it0 >= it1) return;  // (uniform)
+    const uint32_t item = blockIdx.x;  // (launch_pass: one workgroup per item)
 
     Thr c;
     c.lane = threadIdx.x & 63;
@@ -1484,8 +1272,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     c.round = c.qt / Rnd<P, T>::QL;
 
     uint32_t tile, slab;
-    set_item(c, a, it0, G::Q, tile, slab);
-#if !RS16_PIPE
+    set_item(c, a, item, G::Q, tile, slab);
     if constexpr (P == DEC_FIRST) {
         // a tile without received rows is skipped (process_item): return
         // before its table staging and row loads, so its slot frees at once
@@ -1505,7 +1292,6 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     // tables are requested first, the tile's rows right behind them, so the
     // staging latency hides under the row loads.
     stamp(a, 0);
-#if RS16_LDPRIO
     // Load-issue order: the workgroup in slot 0 of its CU (HW_ID.tg_id) issues
     // its rows first, slot 1 next, ...  Same-box A/B: kernel times equal,
     // step time -2 % (643-645 -> 654-659 GiB/s, 3 pairs).  The progress-based
@@ -1516,7 +1302,6 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
         else if (slot == 1) __builtin_amdgcn_s_setprio(2);
         else if (slot == 2) __builtin_amdgcn_s_setprio(1);
     }
-#endif
     TileStage<P, T> st;
     st.issue(a, c);  // twiddle tables first: they do not queue behind the tile
     ItemRegs<P, T> cur;
@@ -1536,27 +1321,6 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     st.finish(a, c, smem);
     stamp(a, 2);
     process_item<P, T>(a, c, tile, slab, cur, smem);
-#else
-    stage_tile<P, T>(a, c, tile, smem);
-    ItemRegs<P, T> nx;
-    load_item<P, T>(a, c, tile, nx);
-    for (uint32_t it = it0; it < it1; it++) {
-        const Thr cc = c;
-        const uint32_t ctile = tile, cslab = slab;
-        ItemRegs<P, T> cur = nx;
-        const bool more = it + 1 < it1;
-        if (more) {
-            set_item(c, a, it + 1, G::Q, tile, slab);
-            load_item<P, T>(a, c, tile, nx);  // in flight during this item's butterflies
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        process_item<P, T>(a, cc, ctile, cslab, cur, smem);
-        if (more && c.b_high != cc.b_high) {
-            __syncthreads();  // every wave is done with this key's tables
-            stage_tile<P, T>(a, c, tile, smem);
-        }
-    }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1592,41 +1356,13 @@ static const int kQuads[9] = {Geo<0>::Q, Geo<1>::Q, Geo<2>::Q, Geo<3>::Q, Geo<4>
                               Geo<5>::Q, Geo<6>::Q, Geo<7>::Q, Geo<8>::Q};
 #undef RS16_TH
 
-// Resident workgroups per CU of the persistent grid (RS16_WG_PER_CU; 0 =
-// one workgroup per item).  Default: RS16_PIPE builds 2 for the 4-wave
-// workgroups of T >= 6 (8 waves and <= 150 KiB of LDS per CU), else 0.
-static int wg_per_cu(int T) {
-    static const int v = [] {
-        const char* e = std::getenv("RS16_WG_PER_CU");
-        return e ? std::atoi(e) : -1;
-    }();
-    if (!RS16_PIPE) return 0;
-    if (v >= 0) return v;
-    return T >= 6 ? 2 : 8;
-}
-static int device_cus() {
-    static int cus[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cus[dev] = n;
-    }
-    return cus[dev];
-}
-
 hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles, hipStream_t s) {
     if (prog < 0 || prog >= NUM_PROGS || T < 0 || T > 8) return hipErrorInvalidValue;
     if (num_tiles == 0 || args.qrow == 0) return hipSuccess;
     PassArgs a = args;
     a.nslab = (a.qrow + kQuads[T] - 1) / kQuads[T];
     a.ntiles = num_tiles;
-    const uint64_t items = (uint64_t)num_tiles * a.nslab;
-    const int wpc = wg_per_cu(T);
-    const uint64_t max_wg = wpc > 0 ? (uint64_t)wpc * device_cus() : items;
-    a.per_wg = (uint32_t)((items + max_wg - 1) / max_wg);
-    const uint32_t nwg = (uint32_t)((items + a.per_wg - 1) / a.per_wg);
+    const uint32_t nwg = num_tiles * a.nslab;  // one workgroup per (tile, slab) item
     if (a.need_hi == 0) a.need_hi = 1u << T;  // no pruning
     {
         const uint64_t hws = kQuads[T] >= 64 ? 1 : 64 / kQuads[T];
@@ -1634,23 +1370,10 @@ hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles
         const uint64_t span = (uint64_t)1 << (T + a.lo);  // rows of one tile's aligned block
         const bool fits = (hws - 1) * ((uint64_t)16 << a.lo) * smax + 1024 < ((uint64_t)1 << 32);
         const bool aligned = a.chunk % span == 0 && a.row_base_in % span == 0;
-        // RS16_FORCE_VOFF64=1 (tests): always the 64-bit lane offsets
-        static const bool force64 = [] {
-            const char* e = std::getenv("RS16_FORCE_VOFF64");
-            return e && e[0] == '1';
-        }();
-        a.voff32 = fits && aligned && !force64 ? 1u : 0u;
+        // (rs16_set_diagnostics RS16_DIAG_FORCE_VOFF64: always the 64-bit lane offsets)
+        a.voff32 = fits && aligned && !(g_diag & DIAG_FORCE_VOFF64) ? 1u : 0u;
     }
-    size_t lds = (size_t)kSmem[prog][T];
-    {
-        // RS16_LDS_PAD_T7=<bytes> (experiment): extra LDS per workgroup of the
-        // T = 7 passes, to cap the resident workgroups per CU
-        static const size_t pad = [] {
-            const char* e = std::getenv("RS16_LDS_PAD_T7");
-            return e ? (size_t)std::atoll(e) : (size_t)0;
-        }();
-        if (T == 7) lds += pad;
-    }
+    const size_t lds = (size_t)kSmem[prog][T];
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)kPass[prog][T], hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);

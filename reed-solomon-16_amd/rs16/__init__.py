@@ -27,11 +27,19 @@ __all__ = [
     "Error", "Engine", "default_engine", "ReedSolomonEncoder", "ReedSolomonDecoder", "RateEncoder",
     "RateDecoder", "EncoderResult", "DecoderResult", "encode", "decode", "encode_device", "decode_device",
     "supports", "validate", "use_high_rate", "encoder_work_count", "decoder_work_count",
-    "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS",
+    "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS", "set_diagnostics",
+    "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL",
 ]
 
 GF_ORDER = 65536
 GF_MODULUS = 65535
+# rs16_set_diagnostics flags (include/rs16.h): alternative code paths for tests
+DIAG_FORCE_VOFF64, DIAG_EVAL_TWO_KERNEL, DIAG_EVAL_FULL = 1, 2, 4
+
+
+def set_diagnostics(flags: int) -> int:
+    """Process-wide diagnostic switches (identical results); returns the previous flags."""
+    return lib().rs16_set_diagnostics(flags)
 RATE_DEFAULT, RATE_HIGH, RATE_LOW = 0, 1, 2
 _RATES = {"default": 0, "high": 1, "low": 2, 0: 0, 1: 1, 2: 2}
 
@@ -303,21 +311,32 @@ def decoder_work_count(high: bool, original_count, recovery_count) -> int:
 # ---------------------------------------------------------------------------
 class EncoderResult:
     """EncoderResult (src/encoder_result.rs).  Dropping it (``del``, ``with``,
-    or ``drop()``) resets the encoder for a new round, like Drop."""
+    or ``drop()``) resets the encoder for a new round, like Drop.  A result
+    that outlives a later round of its encoder (reset, or a new encode after
+    an explicit drop) is stale: its drop is a no-op, as the reference's borrow
+    rules make that state unreachable there."""
 
     def __init__(self, enc: "RateEncoder"):
         self._enc = enc
+        self._gen = enc._gen
+
+    def _live(self) -> "RateEncoder":
+        e = self._enc
+        if e is None or e._gen != self._gen:
+            raise ValueError("EncoderResult used after it was dropped")
+        return e
 
     def recovery(self, index: int) -> Optional[bytes]:
-        e = self._enc
-        buf = C.create_string_buffer(e.shard_bytes)
-        r = lib().rs16_encoder_recovery_copy(e.h, index, buf, e.shard_bytes, C.byref(e._err))
-        if r < 0:
-            raise Error._from_c(e._err)
-        return buf.raw if r == 1 else None
+        e = self._live()
+        p = lib().rs16_encoder_recovery(e.h, index, C.byref(e._err))
+        if not p:
+            if e._err.code != 0:
+                raise Error._from_c(e._err)
+            return None
+        return C.string_at(p, e.shard_bytes)
 
     def recovery_device(self, index: int) -> Optional[int]:
-        return lib().rs16_encoder_recovery_device(self._enc.h, index)
+        return lib().rs16_encoder_recovery_device(self._live().h, index)
 
     def recovery_iter(self) -> Iterator[bytes]:
         i = 0
@@ -330,7 +349,8 @@ class EncoderResult:
 
     def drop(self):
         enc, self._enc = self._enc, None
-        if enc is not None and enc.h:
+        if enc is not None and enc.h and enc._gen == self._gen:
+            enc._gen += 1
             lib().rs16_encoder_result_drop(enc.h)
 
     def __enter__(self):
@@ -347,31 +367,40 @@ class EncoderResult:
 
 
 class DecoderResult:
-    """DecoderResult (src/decoder_result.rs)."""
+    """DecoderResult (src/decoder_result.rs); stale results as EncoderResult."""
 
     def __init__(self, dec: "RateDecoder"):
         self._dec = dec
+        self._gen = dec._gen
+
+    def _live(self) -> "RateDecoder":
+        d = self._dec
+        if d is None or d._gen != self._gen:
+            raise ValueError("DecoderResult used after it was dropped")
+        return d
 
     def restored_original(self, index: int) -> Optional[bytes]:
-        d = self._dec
-        buf = C.create_string_buffer(d.shard_bytes)
-        r = lib().rs16_decoder_restored_original_copy(d.h, index, buf, d.shard_bytes, C.byref(d._err))
-        if r < 0:
-            raise Error._from_c(d._err)
-        return buf.raw if r == 1 else None
+        d = self._live()
+        p = lib().rs16_decoder_restored_original(d.h, index, C.byref(d._err))
+        if not p:
+            if d._err.code != 0:
+                raise Error._from_c(d._err)
+            return None
+        return C.string_at(p, d.shard_bytes)
 
     def restored_original_device(self, index: int) -> Optional[int]:
-        return lib().rs16_decoder_restored_original_device(self._dec.h, index)
+        return lib().rs16_decoder_restored_original_device(self._live().h, index)
 
     def restored_original_iter(self) -> Iterator[Tuple[int, bytes]]:
-        for i in range(self._dec.original_count):
+        for i in range(self._live().original_count):
             r = self.restored_original(i)
             if r is not None:
                 yield i, r
 
     def drop(self):
         dec, self._dec = self._dec, None
-        if dec is not None and dec.h:
+        if dec is not None and dec.h and dec._gen == self._gen:
+            dec._gen += 1
             lib().rs16_decoder_result_drop(dec.h)
 
     def __enter__(self):
@@ -397,6 +426,7 @@ class RateEncoder:
     def __init__(self, original_count, recovery_count, shard_bytes, rate="default", engine: Optional[Engine] = None):
         self.engine = engine or default_engine()
         self._err = RS16Error()
+        self._gen = 0  # bumped by reset() and by a result's drop: older results go stale
         self.h = lib().rs16_encoder_new(self.engine.h, _RATES[rate], original_count, recovery_count, shard_bytes,
                                         C.byref(self._err))
         if not self.h:
@@ -422,6 +452,7 @@ class RateEncoder:
         return bool(lib().rs16_encoder_is_high_rate(self.h))
 
     def reset(self, original_count, recovery_count, shard_bytes):
+        self._gen += 1
         _check(lib().rs16_encoder_reset(self.h, original_count, recovery_count, shard_bytes, C.byref(self._err)),
                self._err)
         self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
@@ -435,6 +466,10 @@ class RateEncoder:
             rc = lib().rs16_encoder_add_original_shard(self.h, p, n, C.byref(self._err))
         _check(rc, self._err)
 
+    def add_original_shard_device(self, d_shard: int, nbytes: int):
+        """add_original_shard with the shard in HBM (raw device pointer)."""
+        _check(lib().rs16_encoder_add_original_shard_device(self.h, d_shard, nbytes, C.byref(self._err)), self._err)
+
     def encode(self) -> EncoderResult:
         _check(lib().rs16_encoder_encode(self.h, C.byref(self._err)), self._err)
         return EncoderResult(self)
@@ -446,6 +481,7 @@ class RateDecoder:
     def __init__(self, original_count, recovery_count, shard_bytes, rate="default", engine: Optional[Engine] = None):
         self.engine = engine or default_engine()
         self._err = RS16Error()
+        self._gen = 0
         self.h = lib().rs16_decoder_new(self.engine.h, _RATES[rate], original_count, recovery_count, shard_bytes,
                                         C.byref(self._err))
         if not self.h:
@@ -469,6 +505,7 @@ class RateDecoder:
         return bool(lib().rs16_decoder_is_high_rate(self.h))
 
     def reset(self, original_count, recovery_count, shard_bytes):
+        self._gen += 1
         _check(lib().rs16_decoder_reset(self.h, original_count, recovery_count, shard_bytes, C.byref(self._err)),
                self._err)
         self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
@@ -489,6 +526,15 @@ class RateDecoder:
 
     def add_recovery_shard(self, index, shard):
         self._add(False, index, shard)
+
+    def add_original_shard_device(self, index, d_shard: int, nbytes: int):
+        """add_original_shard with the shard in HBM (raw device pointer)."""
+        _check(lib().rs16_decoder_add_original_shard_device(self.h, index, d_shard, nbytes, C.byref(self._err)),
+               self._err)
+
+    def add_recovery_shard_device(self, index, d_shard: int, nbytes: int):
+        _check(lib().rs16_decoder_add_recovery_shard_device(self.h, index, d_shard, nbytes, C.byref(self._err)),
+               self._err)
 
     def decode(self) -> DecoderResult:
         _check(lib().rs16_decoder_decode(self.h, C.byref(self._err)), self._err)

@@ -30,6 +30,7 @@ SIGNATURES = {
     "rs16_engine_profile_read": (_i, [_p, _i, C.POINTER(C.c_double), C.POINTER(C.c_uint64), _e]),
     "rs16_engine_profile_reset": (None, [_p]),
     "rs16_prog_count": (_i, []),
+    "rs16_set_diagnostics": (_i, [_i]),
     "rs16_prog_name": (C.c_char_p, [_i]),
     "rs16_engine_set_stamps": (_i, [_p, _p, _i, _e]),
     "rs16_engine_set_slices": (_i, [_p, _i, _e]),
@@ -59,6 +60,7 @@ SIGNATURES = {
     "rs16_encoder_add_original_shard": (_i, [_p, _p, _sz, _e]),
     "rs16_encoder_add_original_shard_device": (_i, [_p, _p, _sz, _e]),
     "rs16_encoder_encode": (_i, [_p, _e]),
+    "rs16_encoder_recovery": (_p, [_p, _sz, _e]),
     "rs16_encoder_recovery_device": (_p, [_p, _sz]),
     "rs16_encoder_recovery_copy": (_i, [_p, _sz, _p, _sz, _e]),
     "rs16_encoder_result_drop": (None, [_p]),
@@ -71,6 +73,7 @@ SIGNATURES = {
     "rs16_decoder_add_original_shard_device": (_i, [_p, _sz, _p, _sz, _e]),
     "rs16_decoder_add_recovery_shard_device": (_i, [_p, _sz, _p, _sz, _e]),
     "rs16_decoder_decode": (_i, [_p, _e]),
+    "rs16_decoder_restored_original": (_p, [_p, _sz, _e]),
     "rs16_decoder_restored_original_device": (_p, [_p, _sz]),
     "rs16_decoder_restored_original_copy": (_i, [_p, _sz, _p, _sz, _e]),
     "rs16_decoder_result_drop": (None, [_p]),

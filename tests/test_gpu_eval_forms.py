@@ -1,12 +1,11 @@
 """Both forms of the decode's eval_poly on block-aligned geometries: the
 one-kernel form (eval_fused_kernel, the default there) runs in this process
 through every aligned decode of the suite; here the two-kernel form
-(fwht_lo_flags_kernel + fwht_hi_mulw_kernel, RS16_EVAL_FUSED=0) runs the same
+(fwht_lo_flags_kernel + fwht_hi_mulw_kernel, rs16.DIAG_EVAL_TWO_KERNEL) runs the same
 decodes in a subprocess.  Both must restore every lost original bit-exactly
 (100 % loss = half-transform decode; tail / scattered losses = general decode
 with lost-range pruning)."""
 import json
-import os
 import subprocess
 import sys
 import textwrap
@@ -24,6 +23,7 @@ SCRIPT = textwrap.dedent("""
     import rs16
     from rs16.device import DeviceArray
     from rs16.util import generate_original
+    rs16.set_diagnostics({flags})
     eng = rs16.default_engine()
     out = []
     for k, m, sb in ((32768, 32768, 64), (4096, 4096, 128), (61440, 4096, 64)):
@@ -54,9 +54,9 @@ SCRIPT = textwrap.dedent("""
 
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_eval_forms_restore(fused):
-    code = SCRIPT.format(pkg=str(ROOT / "reed-solomon-16_amd"), tests=str(ROOT / "tests"))
-    env = dict(os.environ, RS16_EVAL_FUSED=fused)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    flags = 0 if fused == "1" else 2  # rs16.DIAG_EVAL_TWO_KERNEL
+    code = SCRIPT.format(pkg=str(ROOT / "reed-solomon-16_amd"), tests=str(ROOT / "tests"), flags=flags)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1]
     for k, m, pattern, ok in json.loads(line[7:]):

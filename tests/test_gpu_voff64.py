@@ -1,10 +1,9 @@
 """The passes' 64-bit lane-offset address path (PassArgs::voff32 = 0: row
 offsets that do not fit 32 bits, i.e. shards of >= 1 MiB at 65536 rows) is
-forced with RS16_FORCE_VOFF64=1 in a subprocess and checked bit for bit
+forced with rs16.set_diagnostics(DIAG_FORCE_VOFF64) in a subprocess and checked bit for bit
 against the oracle: encode (3 passes), general decode at partial loss and the
 half-transform decode at 100 % original loss, both rates."""
 import json
-import os
 import subprocess
 import sys
 import textwrap
@@ -22,6 +21,7 @@ SCRIPT = textwrap.dedent("""
     import oracle_bind as O
     import rs16
     from rs16.util import generate_original
+    rs16.set_diagnostics(rs16.DIAG_FORCE_VOFF64)
     out = []
     for rate, k, m in (("high", 4096, 4096), ("low", 1000, 3000), ("default", 2000, 2048)):
         sb = 128
@@ -52,8 +52,7 @@ SCRIPT = textwrap.dedent("""
 
 def test_forced_64bit_lane_offsets():
     code = SCRIPT.format(pkg=str(ROOT / "reed-solomon-16_amd"), tests=str(ROOT / "tests"))
-    env = dict(os.environ, RS16_FORCE_VOFF64="1")
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1]
     for rate, *oks in json.loads(line[7:]):

@@ -7,7 +7,12 @@
 using namespace rs16;
 #define ITER 256
 template <int MODE>
-__global__ void __launch_bounds__(256) k(unsigned* out, const unsigned* tab, unsigned seed) {
+__global__ void __launch_bounds__(256) k(unsigned* out, const unsigned* tab, unsigned long long* clk, unsigned seed) {
+    unsigned long long t0 = 0, r0 = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
     unsigned L[16], H[16];
     for (int i = 0; i < 16; i++) { L[i] = seed * (threadIdx.x + i + 1); H[i] = L[i] * 7 + i; }
     unsigned t[20];
@@ -29,32 +34,47 @@ __global__ void __launch_bounds__(256) k(unsigned* out, const unsigned* tab, uns
             asm volatile("" ::: "memory");
         }
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        clk[0] = __builtin_amdgcn_s_memtime() - t0;
+        clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
     unsigned r = 0;
     for (int i = 0; i < 16; i++) r ^= L[i] ^ H[i];
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
+static unsigned long long* g_clk;
+static double g_ghz = 2.4;
 template <int MODE> float run(unsigned* d, const unsigned* tab, int blocks) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
-    k<MODE><<<blocks, 256>>>(d, tab, 1);
+    k<MODE><<<blocks, 256>>>(d, tab, g_clk, 1);
     hipEventRecord(a);
-    k<MODE><<<blocks, 256>>>(d, tab, 1);
+    k<MODE><<<blocks, 256>>>(d, tab, g_clk, 1);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
+    unsigned long long c[2];
+    hipMemcpy(c, g_clk, sizeof c, hipMemcpyDeviceToHost);
+    g_ghz = c[1] ? (double)c[0] / ((double)c[1] * 10.0) : 2.4;
     return ms;
 }
 int main() {
     unsigned* d; unsigned* tab;
     hipMalloc(&d, 256 * 16 * 256 * 4);
     hipMalloc(&tab, 8 * 32 * 4);
+    hipMalloc(&g_clk, 16);
     hipMemset(tab, 0x5a, 8 * 32 * 4);
     for (int wps = 1; wps <= 8; wps *= 2) {
         int blocks = 256 * wps;  // 256-thread blocks = 1 wave per SIMD each
         float ms0 = run<0>(d, tab, blocks), ms1 = run<1>(d, tab, blocks);
         double bf = (double)blocks * 4 * ITER * 32;  // wave-butterflies
-        printf("waves/SIMD %d: FFT %.3f ms (%.1f cyc/wave-bfly/SIMD)  IFFT %.3f ms (%.1f)\n", wps, ms0,
-               ms0 * 1e-3 * 2.4e9 * 1024 / bf, ms1, ms1 * 1e-3 * 2.4e9 * 1024 / bf);
+        const double g0 = g_ghz;
+        float ms1b = run<1>(d, tab, blocks);
+        const double g1 = g_ghz;
+        (void)ms1;
+        printf("waves/SIMD %d: FFT %.3f ms @ %.2f GHz (%.1f cyc/wave-bfly/SIMD = %.2f per instr of 30)  IFFT %.3f ms @ %.2f GHz (%.1f)\n",
+               wps, ms0, g0, ms0 * 1e-3 * g0 * 1e9 * 1024 / bf, ms0 * 1e-3 * g0 * 1e9 * 1024 / bf / 30, ms1b, g1,
+               ms1b * 1e-3 * g1 * 1e9 * 1024 / bf);
     }
     return 0;
 }
