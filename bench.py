@@ -219,6 +219,91 @@ def api_reference_loop(S, seconds):
     return out
 
 
+def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
+    """BASELINE configs[4]: one 32768:32768 x 64 KiB stripe resident in rank
+    0's HBM, byte-column partitioned across the ranks with RCCL over xGMI
+    (rs16_scatter_columns / rs16_gather_columns, include/rs16.h): scatter the
+    originals' column slices, every rank encodes its slice, gather the
+    recovery slices; then scatter the recovery, every rank decodes its slice
+    at 100 % original loss, gather the restored originals.  Timed end to end
+    (barrier + max over ranks) and as codec only / collectives only.  At one
+    rank the collectives are the root's pack / unpack copies and a send to
+    itself; the whole-stripe restore is checked on rank 0."""
+    import numpy as np
+
+    import rs16
+    from rs16.device import DeviceArray
+
+    S4 = 65536
+    if world == 1:
+        (comm,) = rs16.Comm.init_all([eng])
+    else:
+        import torch
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid[:] = torch.frombuffer(bytearray(rs16.Comm.unique_id()), dtype=torch.uint8)
+        dist.broadcast(uid, 0)
+        comm = rs16.Comm(eng, world, rank, bytes(uid.numpy().tobytes()))
+    off, w = rs16.column_slice(S4, world, rank)
+    root = rank == 0
+    d_orig = d_rec = d_out = None
+    if root:
+        orig = np.frombuffer(np.random.default_rng(4).bytes(k * S4), np.uint8).reshape(k, S4)
+        d_orig = DeviceArray.from_numpy(eng, orig)
+        d_rec, d_out = DeviceArray(eng, m * S4), DeviceArray(eng, k * S4)
+    d_os, d_rs = DeviceArray(eng, k * w), DeviceArray(eng, m * w)
+    d_ds = DeviceArray(eng, k * w)
+    of = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+    rf = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+    full = lambda d: [d.ptr if d is not None else 0]
+
+    def scatter_orig():
+        rs16.scatter_columns([comm], 0, k, S4, full(d_orig), [d_os.ptr])
+
+    def gather_rec():
+        rs16.gather_columns([comm], 0, m, S4, [d_rs.ptr], full(d_rec))
+
+    def scatter_rec():
+        rs16.scatter_columns([comm], 0, m, S4, full(d_rec), [d_rs.ptr])
+
+    def gather_out():
+        rs16.gather_columns([comm], 0, k, S4, [d_ds.ptr], full(d_out))
+
+    def codec():
+        rs16.encode_device(k, m, w, d_os.ptr, d_rs.ptr, engine=eng)
+        rs16.decode_device(k, m, w, d_ds.ptr, of.ptr, d_rs.ptr, rf.ptr, 0, m, engine=eng)
+
+    def step():
+        scatter_orig()
+        rs16.encode_device(k, m, w, d_os.ptr, d_rs.ptr, engine=eng)
+        gather_rec()
+        scatter_rec()
+        rs16.decode_device(k, m, w, d_ds.ptr, of.ptr, d_rs.ptr, rf.ptr, 0, m, engine=eng)
+        gather_out()
+
+    step()
+    barrier()
+    ok = None
+    if root:
+        ok = bool(np.array_equal(d_out.download(shape=(k, S4)), orig))
+        assert ok, "configs[4] via RCCL: decode did not restore the stripe"
+    step()
+    n4 = max(3, steps // 4)
+    t_all = timed(step, n4)
+    t_codec = timed(codec, n4)
+    t_coll = timed(lambda: (scatter_orig(), gather_rec(), scatter_rec(), gather_out()), n4)
+    comm.close()
+    step_bytes = 2 * (k + m) * S4
+    return {
+        "workload": f"{k}:{m} x {S4} B stripe in rank 0's HBM, byte columns split over {world} rank(s) "
+                    f"({w} B each) with RCCL scatter/gather; encode + 100%-loss decode (BASELINE configs[4])",
+        "gib_s": step_bytes * n4 / t_all / GIB, "ms_per_step": t_all / n4 * 1e3,
+        "codec_only_gib_s": step_bytes * n4 / t_codec / GIB, "codec_only_ms": t_codec / n4 * 1e3,
+        "collectives_ms": t_coll / n4 * 1e3,
+        "collective_bytes_per_step": 4 * (k * S4 - k * w) if world > 1 else 0,
+        "restored_stripe_verified": ok, "whole_configs4": world == 8}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -421,29 +506,7 @@ def main():
                                      "received": f"originals 0..{k - L1}, recovery 0..{L1}"}
 
     if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
-        # BASELINE configs[4] (32768:32768 x 64 KiB over 8 GPUs): one rank's
-        # share, an 8 KiB column slice of every shard, measured on this GPU
-        # (random bytes; the decode must restore every original)
-        S4 = 65536 // 8
-        o4 = np.random.default_rng(seed).integers(0, 256, (k, S4), dtype=np.uint8)
-        a4 = DeviceArray.from_numpy(eng, o4)
-        r4, x4 = DeviceArray(eng, m * S4), DeviceArray(eng, k * S4)
-        e4 = lambda: rs16.encode_device(k, m, S4, a4.ptr, r4.ptr, engine=eng)
-        d4 = lambda: rs16.decode_device(k, m, S4, x4.ptr, d_of.ptr, r4.ptr, d_rf.ptr, k - loss, loss, engine=eng)
-        e4()
-        d4()
-        assert np.array_equal(x4.download(shape=(k, S4)), o4), "configs[4] share: decode did not restore"
-        for _ in range(2):
-            e4(); d4()
-        n4 = max(3, args.steps // 4)
-        t4 = timed(lambda: (e4(), d4()), n4)
-        # (timed(): barrier + max over ranks; at 8 ranks this is configs[4] itself)
-        extra["configs4_column_slices"] = {
-            "workload": f"{k}:{m} x 65536 B split into 8 column slices of {S4} B (BASELINE configs[4]); "
-                        f"{world} slice(s) here, one per rank, encode + 100%-loss decode, no collective",
-            "gib_s": world * 2 * (k + m) * S4 * n4 / t4 / GIB, "per_rank_gib_s": 2 * (k + m) * S4 * n4 / t4 / GIB,
-            "ms_per_step": t4 / n4 * 1e3, "whole_configs4": world == 8}
-        del a4, r4, x4
+        extra["configs4_rccl"] = configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, args.steps)
 
     if not args.no_extra and world == 1:
         # Serving mode (not the metric): two independent stripes per step, one

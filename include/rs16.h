@@ -56,7 +56,7 @@ typedef enum rs16_error_code {
     RS16_TOO_MANY_ORIGINAL_SHARDS = 9,       /* v0 original_count */
     RS16_UNSUPPORTED_SHARD_COUNT = 10,       /* v0 original_count, v1 recovery_count */
     /* Not in the reference (it has no device and panics on misuse): */
-    RS16_DEVICE_ERROR = 100,                 /* HIP runtime failure, v0 = hipError_t */
+    RS16_DEVICE_ERROR = 100,                 /* HIP runtime failure, v0 = hipError_t (RCCL: 1000 + ncclResult_t) */
     RS16_INVALID_ARGUMENT = 101              /* engine-op misuse the reference would panic on */
 } rs16_error_code;
 
@@ -253,6 +253,52 @@ int rs16_decode_host(rs16_engine* eng, size_t original_count, size_t recovery_co
                      void* h_original, const uint8_t* original_received, const void* h_recovery,
                      const uint8_t* recovery_received, size_t slice_bytes, rs16_error* err);
 
+/* ---- Several GPUs in one process ------------------------
+ * reed_solomon_16::encode / decode of ONE stripe with host-resident shards,
+ * its byte columns split over the n engines (one per GPU): engine j takes its
+ * share of the B = shard_bytes / 64 column blocks (rs16_column_slice; every
+ * column block is an independent codeword, src/algorithm.md:18-32), copies
+ * them in with a pitched DMA copy, runs the device codec and copies them
+ * back; the engines run concurrently, with no exchange between the GPUs.
+ * Synchronous.  Results are identical to rs16_encode_host / rs16_decode_host
+ * (n = 1 is that call with one whole-width slice).  Decode: host flag byte
+ * arrays; lost originals restored in place into h_original. */
+int rs16_encode_host_multi(rs16_engine* const* engines, int n, size_t original_count, size_t recovery_count,
+                           size_t shard_bytes, const void* h_original, void* h_recovery, rs16_error* err);
+int rs16_decode_host_multi(rs16_engine* const* engines, int n, size_t original_count, size_t recovery_count,
+                           size_t shard_bytes, void* h_original, const uint8_t* original_received,
+                           const void* h_recovery, const uint8_t* recovery_received, rs16_error* err);
+
+/* ---- RCCL over xGMI: column-slice scatter / gather -----
+ * For a stripe that lives in ONE GPU's HBM (BASELINE configs[4]): the root's
+ * rows x shard_bytes array is split into byte-column slices, rank r getting
+ * whole 64-byte column blocks, B / n of them and one more for the first
+ * B mod n ranks (B = shard_bytes / 64; rs16_column_slice), as a contiguous
+ * rows x width array -- itself a shard
+ * array of shard_bytes = width, so every rank runs the device codec on its
+ * slice with no further exchange -- and gathered back the same way.  The
+ * root packs / unpacks with pitched device copies; the slices move with one
+ * grouped ncclSend / ncclRecv per rank.  Ranks are processes (one
+ * rs16_comm_new each, with the root's rs16_comm_unique_id shared out of
+ * band) or engines of one process (rs16_comm_init_all).  The collective
+ * calls take this process's communicators (n of them, ranks in any order)
+ * with one buffer per communicator: d_full is used on the root only,
+ * d_slice on every rank.  Asynchronous on `stream` (n == 1) or on each
+ * engine's stream. */
+typedef struct rs16_comm rs16_comm;
+int rs16_comm_unique_id(void* id128, rs16_error* err);
+rs16_comm* rs16_comm_new(rs16_engine* eng, int nranks, int rank, const void* id128, rs16_error* err);
+int rs16_comm_init_all(rs16_engine* const* engines, int n, rs16_comm** comms, rs16_error* err);
+void rs16_comm_free(rs16_comm* comm);
+int rs16_comm_rank(const rs16_comm* comm);
+int rs16_comm_size(const rs16_comm* comm);
+/* Column slice of `rank` among `nranks`: byte offset and width (multiples of 64; width may be 0). */
+int rs16_column_slice(size_t shard_bytes, int nranks, int rank, size_t* offset, size_t* width);
+int rs16_scatter_columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t shard_bytes,
+                         const void* const* d_full, void* const* d_slice, void* stream, rs16_error* err);
+int rs16_gather_columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t shard_bytes,
+                        const void* const* d_slice, void* const* d_full, void* stream, rs16_error* err);
+
 /* ---- Device memory helpers (so FFI callers need no HIP headers) ------- */
 void* rs16_device_alloc(rs16_engine* eng, size_t bytes, rs16_error* err);
 void rs16_device_free(rs16_engine* eng, void* d_ptr);
@@ -263,7 +309,8 @@ int rs16_memset_device(rs16_engine* eng, void* d_dst, int value, size_t bytes, v
  * without HIP headers that run codecs on streams of their own. */
 void* rs16_stream_create(rs16_engine* eng, rs16_error* err);
 void rs16_stream_destroy(rs16_engine* eng, void* stream);
-/* Page-locked host staging memory (hipHostMalloc): shards that start and end
+/* Page-locked host staging memory (hipHostMalloc, portable: usable by every
+ * engine of a multi-GPU call): shards that start and end
  * in host memory move over PCIe at DMA rate from/to these buffers (the
  * host-resident path of EncoderWork / DecoderWork, src/rate/encoder_work.rs:49-69). */
 void* rs16_host_alloc(rs16_engine* eng, size_t bytes, rs16_error* err);

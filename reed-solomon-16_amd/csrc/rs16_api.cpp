@@ -966,6 +966,113 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
     return set_error(err, RS16_OK);
 }
 
+// ---------------------------------------------------------------------------
+// Several GPUs in one process: the byte columns of one stripe are split over
+// the engines (every 64-byte column block is an independent codeword,
+// src/algorithm.md:18-32); each engine copies its column
+// slice in with a pitched DMA copy, runs the device codec on it and copies
+// it back, all engines concurrently.  No exchange between the GPUs.
+// ---------------------------------------------------------------------------
+// Column slice of engine j of n: rs16_column_slice (rs16_comm.cpp), the
+// partition the RCCL scatter / gather and rs16/columns.py use.
+static void multi_slice(size_t S, int n, int j, size_t* off, size_t* w) { (void)rs16_column_slice(S, n, j, off, w); }
+static int multi_check(rs16_engine* const* engines, int n, rs16_error* err) {
+    if (!engines || n < 1) return set_error(err, RS16_INVALID_ARGUMENT);
+    for (int j = 0; j < n; j++)
+        if (!engines[j]) return set_error(err, RS16_INVALID_ARGUMENT);
+    return RS16_OK;
+}
+static int multi_sync(rs16_engine* const* engines, int n, rs16_error* err) {
+    for (int j = 0; j < n; j++) {
+        rs16_engine* e = engines[j];
+        if (int rc = e->activate(err)) return rc;
+        RS16_HIP(hipStreamSynchronize(e->stream));
+        if (int rc = e->scratch_done(e->stream, err)) return rc;
+    }
+    return RS16_OK;
+}
+
+extern "C" int rs16_encode_host_multi(rs16_engine* const* engines, int n, size_t k, size_t m, size_t S,
+                                      const void* h_original, void* h_recovery, rs16_error* err) {
+    if (int rc = multi_check(engines, n, err)) return rc;
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    const size_t wc = rs16_encoder_work_count(high, k, m);
+    for (int j = 0; j < n; j++) {
+        size_t off, w;
+        multi_slice(S, n, j, &off, &w);
+        if (w == 0) continue;
+        rs16_engine* e = engines[j];
+        if (int rc = e->activate(err)) return rc;
+        if (int rc = e->order(e->stream, err)) return rc;
+        auto& sl = e->hslot[0];
+        RS16_HIP(sl.orig.reserve(k * w));
+        RS16_HIP(sl.rec.reserve(m * w));
+        RS16_HIP(sl.z.reserve(wc * w));
+        RS16_HIP(hipMemcpy2DAsync(sl.orig.p, w, (const uint8_t*)h_original + off, S, w, k, hipMemcpyHostToDevice,
+                                  e->stream));
+        if (int rc = encode_dev(e, high, k, m, w, (const uint8_t*)sl.orig.p, (uint8_t*)sl.rec.p, (uint8_t*)sl.z.p,
+                                e->stream, err))
+            return rc;
+        RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_recovery + off, S, sl.rec.p, w, w, m, hipMemcpyDeviceToHost,
+                                  e->stream));
+    }
+    if (int rc = multi_sync(engines, n, err)) return rc;
+    return set_error(err, RS16_OK);
+}
+
+extern "C" int rs16_decode_host_multi(rs16_engine* const* engines, int n, size_t k, size_t m, size_t S,
+                                      void* h_original, const uint8_t* original_received, const void* h_recovery,
+                                      const uint8_t* recovery_received, rs16_error* err) {
+    if (int rc = multi_check(engines, n, err)) return rc;
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    size_t orig_recv = 0, rec_recv = 0;
+    for (size_t i = 0; i < k; i++) orig_recv += original_received[i] != 0;
+    for (size_t i = 0; i < m; i++) rec_recv += recovery_received[i] != 0;
+    if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
+    if (orig_recv == k) return set_error(err, RS16_OK);
+    DecodeGeom g = decode_geom(high, k, m);
+    g.a_recv = high ? rec_recv : orig_recv;
+    g.b_recv = high ? orig_recv : rec_recv;
+    for (int j = 0; j < n; j++) {
+        size_t off, w;
+        multi_slice(S, n, j, &off, &w);
+        if (w == 0) continue;
+        rs16_engine* e = engines[j];
+        if (int rc = e->activate(err)) return rc;
+        if (int rc = e->order(e->stream, err)) return rc;
+        auto& sl = e->hslot[0];
+        RS16_HIP(sl.orig.reserve(k * w));
+        RS16_HIP(sl.rec.reserve(m * w));
+        RS16_HIP(sl.z.reserve((size_t)g.n * w));
+        RS16_HIP(sl.u.reserve((size_t)g.n * w));
+        RS16_HIP(e->hflags.reserve(k + m));
+        uint8_t* d_of = (uint8_t*)e->hflags.p;
+        uint8_t* d_rf = d_of + k;
+        RS16_HIP(hipMemcpyAsync(d_of, original_received, k, hipMemcpyHostToDevice, e->stream));
+        RS16_HIP(hipMemcpyAsync(d_rf, recovery_received, m, hipMemcpyHostToDevice, e->stream));
+        const uint8_t* fa = high ? d_rf : d_of;
+        const uint8_t* fb = high ? d_of : d_rf;
+        if (int rc = e->decode_eval(g, fa, fb, e->stream, err)) return rc;
+        if (rec_recv)
+            RS16_HIP(hipMemcpy2DAsync(sl.rec.p, w, (const uint8_t*)h_recovery + off, S, w, m, hipMemcpyHostToDevice,
+                                      e->stream));
+        if (orig_recv)
+            RS16_HIP(hipMemcpy2DAsync(sl.orig.p, w, (const uint8_t*)h_original + off, S, w, k, hipMemcpyHostToDevice,
+                                      e->stream));
+        const uint8_t* o = (const uint8_t*)sl.orig.p;
+        const uint8_t* r = (const uint8_t*)sl.rec.p;
+        if (int rc = e->decode_passes(g, w, w, high ? r : o, fa, high ? o : r, fb, (uint8_t*)sl.orig.p,
+                                      (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, e->stream, err))
+            return rc;
+        RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_original + off, S, sl.orig.p, w, w, k, hipMemcpyDeviceToHost,
+                                  e->stream));
+    }
+    if (int rc = multi_sync(engines, n, err)) return rc;
+    return set_error(err, RS16_OK);
+}
+
 extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, void* d_original,
                                   const uint8_t* d_original_received, const void* d_recovery,
                                   const uint8_t* d_recovery_received, size_t orig_recv, size_t rec_recv, void* stream,
@@ -1047,7 +1154,7 @@ extern "C" void rs16_stream_destroy(rs16_engine* e, void* st) {
 extern "C" void* rs16_host_alloc(rs16_engine* e, size_t bytes, rs16_error* err) {
     if (e->activate(err)) return nullptr;
     void* p = nullptr;
-    hipError_t he = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    hipError_t he = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable);
     if (he != hipSuccess) return hip_fail(err, he), nullptr;
     set_error(err, RS16_OK);
     return p;

@@ -30,7 +30,7 @@ hipError_t HostBuf::reserve(size_t bytes) {
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocPortable);
     if (e == hipSuccess) cap = bytes;
     return e;
 }

@@ -558,7 +558,7 @@ template <int NR> __device__ __forceinline__ void pin_rows(uint32_t (&L)[NR], ui
 //   PR_ZERO IFFT: a group whose rows are all zero on input stays zero and is
 //           skipped.  zmask bit j = tile rows [16j, 16j+16) are all zero.
 enum { PR_NONE = 0, PR_OUT, PR_ZERO };
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, int G, class FIN = NoFin>
+template <int P, int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE, int G, class FIN = NoFin>
 struct GroupLoop {
     static __device__ __forceinline__ void run(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                                const PassArgs& a, const uint4* tab1, const uint4* tab2,
@@ -581,7 +581,20 @@ struct GroupLoop {
             constexpr uint32_t all = (uint32_t)((1ull << nb) - 1);
             need = ((zmask >> (gi * nb)) & all) != all;
         }
-        if (need) {
+        // Zero twiddle (the reference's GF_MODULUS sentinel: XOR only, no
+        // multiply, engine_naive.rs:64,116).  The sentinel skew entries are
+        // exactly the indices 2^i - 1 (rs16_tables.cpp checks this when it
+        // builds the tables), which only the first group of a layer-B layer
+        // can hit (index = b_high 2^(lo+T) + (2 gi + 1) 2^(lo+kb) + skew - 1):
+        // ENC_MID's FFT half and the half decode's IFFT half (skew 0, b_high
+        // 0) skip 15 of their 128 multiplies per row set this way.  Layout-B
+        // twiddles are uniform, so this is a uniform branch.
+        bool mul = true;
+        if constexpr (LB && gi == 0 && ProgTraits<P>::IFFT && ProgTraits<P>::FFT) {
+            const uint32_t idx = (c.b_high << (a.lo + T)) + (1u << (a.lo + kb)) + (FFT ? a.skew_fft : a.skew_ifft) - 1;
+            mul = (idx & (idx + 1)) != 0;
+        }
+        if (need && mul) {
 #pragma unroll
             for (int j = 0; j < (1 << rb); j++) {
                 const int m = (gi << (rb + 1)) + j, m2 = m + (1 << rb);
@@ -595,24 +608,31 @@ struct GroupLoop {
                     mul_xor(L[m], H[m], L[m2], H[m2], cur);
                 }
             }
+        } else if (need) {
+#pragma unroll
+            for (int j = 0; j < (1 << rb); j++) {
+                const int m = (gi << (rb + 1)) + j, m2 = m + (1 << rb);
+                L[m2] ^= L[m];
+                H[m2] ^= H[m];
+            }
         }
         pin_rows<Geo<T>::NR>(L, H);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (S::DF && kb == 0) fin(L, H, gi << 1);  // rows 2 gi, 2 gi + 1 are final
         if constexpr (more)
-            GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, G + 1, FIN>::run(L, H, c, a, tab1, tab2, nxt, zmask, fin);
+            GroupLoop<P, T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, G + 1, FIN>::run(L, H, c, a, tab1, tab2, nxt, zmask, fin);
     }
 };
 
 // Apply the layers for k-bits [KB0, KB1) held in registers of layout LB.
-template <int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE = PR_NONE, class FIN = NoFin>
+template <int P, int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE = PR_NONE, class FIN = NoFin>
 __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                        const PassArgs& a, const uint4* tab1, const uint4* tab2,
                                        uint32_t zmask = 0, const FIN& fin = FIN()) {
     if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6)) {
         uint32_t t0[20];
         load_table_lds(t0, group_table<T, LB, KB0, KB1, FFT, 0, IN_TAB2>(c, tab1, tab2));
-        GroupLoop<T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0, FIN>::run(L, H, c, a, tab1, tab2, t0, zmask, fin);
+        GroupLoop<P, T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0, FIN>::run(L, H, c, a, tab1, tab2, t0, zmask, fin);
     }
 }
 
@@ -1160,7 +1180,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         // DEC_MID: a wave whose rows all are zero skips its layout-A layers
         bool skip_a = false;
         if constexpr (ZERO_SKIP) skip_a = __all(d.zrow == (1u << NR) - 1);
-        if (!skip_a) layers<T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
+        if (!skip_a) layers<P, T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
         stamp(a, 3);
         prio<P, 1>();
         if constexpr (T > 4) {
@@ -1170,7 +1190,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                 if constexpr (LateS2<P, T>::value) s3.commit((uint4*)(smem + SM::TAB1_OFF));
             });
             stamp(a, 4);
-            layers<T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
+            layers<P, T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
                                                                                                 tab2, d.zmask);
             in_b = true;
         }
@@ -1186,7 +1206,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     // ---------------- FFT ----------------
     if constexpr (PT::FFT) {
         if constexpr (T > 4) {
-            layers<T, true, R, (T > 4 ? T : R), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
+            layers<P, T, true, R, (T > 4 ? T : R), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
             stamp(a, 7);
             prio<P, 3>();
@@ -1214,10 +1234,10 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         if constexpr (EARLY) {
             Thr cs = c;
             asm volatile("" : "+v"(cs.offL));
-            layers<T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2, 0,
+            layers<P, T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2, 0,
                                                                    EarlyStore<P, T>{a, cs, rvt, lostf});
         } else if (need) {
-            layers<T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2);
+            layers<P, T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2);
         }
         stamp(a, 9);
     }

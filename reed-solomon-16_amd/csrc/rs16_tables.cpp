@@ -8,6 +8,8 @@
 //   LogWalsh = FWHT(log) with log[0] = 0 (src/engine/tables.rs:127-139).
 // The device-side multiply tables are a GPU-specific format (v_perm byte
 // tables, rs16_gf.hpp), not the reference's Mul16 nibble tables.
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -85,6 +87,15 @@ void build(HostTables& t) {
     t.log_walsh[0] = 0;
     fwht_full(t.log_walsh);
 
+    // The pass kernels skip the multiply of uniform groups whose twiddle is
+    // the sentinel and recognise those by index: the sentinel entries are
+    // exactly the indices 2^i - 1 (rs16_pass.hip, GroupLoop).  A table that
+    // broke this would give wrong results, so it is checked here, once.
+    for (uint32_t i = 0; i < GF_MODULUS; i++)
+        if ((t.skew[i] == GF_MODULUS) != ((i & (i + 1)) == 0)) {
+            fprintf(stderr, "rs16: skew table sentinel at unexpected index %u\n", i);
+            abort();
+        }
     // FFT/IFFT twiddle table *entries*: sentinel GF_MODULUS -> ZERO_ENTRY.
     t.skew_entry.assign(GF_ORDER, ZERO_ENTRY);
     for (uint32_t i = 0; i < GF_MODULUS; i++) t.skew_entry[i] = t.skew[i] == GF_MODULUS ? ZERO_ENTRY : t.skew[i];

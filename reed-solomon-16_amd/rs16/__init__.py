@@ -28,7 +28,8 @@ __all__ = [
     "RateDecoder", "EncoderResult", "DecoderResult", "encode", "decode", "encode_device", "decode_device",
     "supports", "validate", "use_high_rate", "encoder_work_count", "decoder_work_count",
     "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS", "set_diagnostics",
-    "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL",
+    "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL", "encode_host", "decode_host",
+    "encode_host_multi", "decode_host_multi", "Comm", "column_slice", "scatter_columns", "gather_columns",
 ]
 
 GF_ORDER = 65536
@@ -648,3 +649,107 @@ def decode_host(original_count, recovery_count, shard_bytes, h_original, origina
     _check(lib().rs16_decode_host(eng.h, original_count, recovery_count, shard_bytes, _host_ptr(h_original),
                                   _host_ptr(original_received), _host_ptr(h_recovery),
                                   _host_ptr(recovery_received), slice_bytes, C.byref(err)), err)
+
+
+def _engine_array(engines):
+    arr = (C.c_void_p * len(engines))(*[e.h for e in engines])
+    return arr
+
+
+def encode_host_multi(original_count, recovery_count, shard_bytes, h_original, h_recovery, engines):
+    """One stripe with host-resident shards, byte columns split over several
+    engines (one per GPU) that run concurrently (rs16_encode_host_multi)."""
+    err = RS16Error()
+    _check(lib().rs16_encode_host_multi(_engine_array(engines), len(engines), original_count, recovery_count,
+                                        shard_bytes, _host_ptr(h_original), _host_ptr(h_recovery), C.byref(err)), err)
+
+
+def decode_host_multi(original_count, recovery_count, shard_bytes, h_original, original_received, h_recovery,
+                      recovery_received, engines):
+    """rs16_decode_host_multi: lost originals restored in place into h_original."""
+    err = RS16Error()
+    _check(lib().rs16_decode_host_multi(_engine_array(engines), len(engines), original_count, recovery_count,
+                                        shard_bytes, _host_ptr(h_original), _host_ptr(original_received),
+                                        _host_ptr(h_recovery), _host_ptr(recovery_received), C.byref(err)), err)
+
+
+# ---------------------------------------------------------------------------
+# RCCL over xGMI: byte-column scatter / gather of a stripe held by one GPU
+# (include/rs16.h "RCCL over xGMI"; SURVEY.md 8(e), BASELINE configs[4])
+# ---------------------------------------------------------------------------
+def column_slice(shard_bytes: int, nranks: int, rank: int) -> Tuple[int, int]:
+    """(byte offset, width) of rank's column slice: whole 64-byte blocks, the
+    first (B mod n) ranks one block more (as rs16/columns.py)."""
+    off, w = C.c_size_t(), C.c_size_t()
+    if lib().rs16_column_slice(shard_bytes, nranks, rank, C.byref(off), C.byref(w)) != 0:
+        raise Error("InvalidArgument")
+    return off.value, w.value
+
+
+class Comm:
+    """One rank's RCCL communicator bound to an engine (rs16_comm)."""
+
+    def __init__(self, engine: Engine, nranks: int = 0, rank: int = 0, unique_id: bytes = b"", _h=None):
+        self.engine = engine
+        self._err = RS16Error()
+        if _h is not None:
+            self.h = _h
+        else:
+            buf = C.create_string_buffer(bytes(unique_id), 128)
+            self.h = lib().rs16_comm_new(engine.h, nranks, rank, buf, C.byref(self._err))
+            if not self.h:
+                raise Error._from_c(self._err)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """The root's ncclUniqueId (128 bytes), to be shared with every rank."""
+        buf = C.create_string_buffer(128)
+        err = RS16Error()
+        _check(lib().rs16_comm_unique_id(buf, C.byref(err)), err)
+        return buf.raw
+
+    @classmethod
+    def init_all(cls, engines) -> list:
+        """One communicator per engine of this process (ncclCommInitAll)."""
+        arr = (C.c_void_p * len(engines))()
+        err = RS16Error()
+        _check(lib().rs16_comm_init_all(_engine_array(engines), len(engines), arr, C.byref(err)), err)
+        return [cls(e, _h=arr[i]) for i, e in enumerate(engines)]
+
+    @property
+    def rank(self) -> int:
+        return lib().rs16_comm_rank(self.h)
+
+    @property
+    def size(self) -> int:
+        return lib().rs16_comm_size(self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rs16_comm_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _ptrs(xs):
+    return (C.c_void_p * len(xs))(*[int(x or 0) for x in xs])
+
+
+def scatter_columns(comms, root, rows, shard_bytes, d_full, d_slice, stream=None):
+    """Root's rows x shard_bytes array (d_full[i] of the root's comm) -> every
+    rank's contiguous rows x width column slice (d_slice[i])."""
+    err = RS16Error()
+    _check(lib().rs16_scatter_columns((C.c_void_p * len(comms))(*[c.h for c in comms]), len(comms), root, rows,
+                                      shard_bytes, _ptrs(d_full), _ptrs(d_slice), stream, C.byref(err)), err)
+
+
+def gather_columns(comms, root, rows, shard_bytes, d_slice, d_full, stream=None):
+    """Every rank's column slice -> the root's rows x shard_bytes array."""
+    err = RS16Error()
+    _check(lib().rs16_gather_columns((C.c_void_p * len(comms))(*[c.h for c in comms]), len(comms), root, rows,
+                                     shard_bytes, _ptrs(d_slice), _ptrs(d_full), stream, C.byref(err)), err)

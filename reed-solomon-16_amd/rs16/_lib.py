@@ -88,6 +88,17 @@ SIGNATURES = {
     "rs16_encode_host": (_i, [_p, _sz, _sz, _sz, _p, _p, _sz, _e]),
     "rs16_decode_host": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _p, _sz, _e]),
     "rs16_host_alloc": (_p, [_p, _sz, _e]),
+    "rs16_comm_unique_id": (_i, [_p, _e]),
+    "rs16_comm_new": (_p, [_p, _i, _i, _p, _e]),
+    "rs16_comm_init_all": (_i, [_p, _i, _p, _e]),
+    "rs16_comm_free": (None, [_p]),
+    "rs16_comm_rank": (_i, [_p]),
+    "rs16_comm_size": (_i, [_p]),
+    "rs16_column_slice": (_i, [_sz, _i, _i, C.POINTER(_sz), C.POINTER(_sz)]),
+    "rs16_scatter_columns": (_i, [_p, _i, _i, _sz, _sz, _p, _p, _p, _e]),
+    "rs16_gather_columns": (_i, [_p, _i, _i, _sz, _sz, _p, _p, _p, _e]),
+    "rs16_encode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _e]),
+    "rs16_decode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _p, _p, _e]),
     "rs16_stream_create": (_p, [_p, _e]),
     "rs16_stream_destroy": (None, [_p, _p]),
     "rs16_host_free": (None, [_p, _p]),

@@ -178,3 +178,19 @@ def test_host_mul_all_logs_one_block():
         O.mul(want, log_m, "nosimd")
         lib().rs16_host_mul(x.ctypes.data_as(C.c_void_p), got.ctypes.data_as(C.c_void_p), 64, log_m)
         assert np.array_equal(got, want), log_m
+
+
+def test_column_slice_partition_matches_python():
+    # rs16_column_slice (the RCCL scatter / gather and multi-engine split) and
+    # rs16/columns.py (the bench's per-rank split) partition alike: every
+    # 64-byte block once, in order (src/algorithm.md:18-32)
+    from rs16.columns import column_slices
+    for S in (64, 192, 1024, 64 * 1024, 64 * 5):
+        for n in (1, 2, 3, 4, 8):
+            got = [rs16.column_slice(S, n, r) for r in range(n)]
+            assert sum(w for _, w in got) == S
+            assert all(o % 64 == 0 and w % 64 == 0 for o, w in got)
+            assert [o for o, _ in got] == sorted(o for o, _ in got)
+            assert got == column_slices(S, n)
+    with pytest.raises(rs16.Error):
+        rs16.column_slice(100, 2, 0)
