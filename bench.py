@@ -440,9 +440,15 @@ def main():
                 "whole_step_frac": round(step_bytes / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
 
     # The passes are bound by VALU issue, not HBM: the
-    # same kernel against the VALU ceiling of this GF(2^16) butterfly (a quad
-    # of 4 elements = 30 VALU instructions: 12 v_perm_b32 lookups, 10 selector
-    # ops, 6 v_bitop3 XORs, 2 XORs), at 1024 SIMDs x 16 lanes x 2.4 GHz peak
+    # same kernel against the VALU ceiling of this GF(2^16) butterfly.  A
+    # wave-quad-butterfly (4 elements per lane: 12 v_perm_b32, 10 selector
+    # ops, 6 v_bitop3_b32, 2 XORs = 30 VALU instructions) measured 115.7
+    # SIMD cycles at 8 waves per SIMD (119.9 at 4; tools/ubench_bfly.hip,
+    # profiles/r03_ubench_bfly.txt): v_perm_b32 issues every ~4.2 cycles at
+    # any occupancy and any stream that mixes it with single-rate ops runs at
+    # ~4 cycles per instruction (profiles/r03_ubench_mix.txt), although those
+    # ops alone issue every ~2.5 (profiles/r03_ubench_valu.txt).  Ceiling =
+    # 1024 SIMDs x 256 element-butterflies / 115.7 cycles at the 2.4 GHz peak
     # clock.  Algorithmic work = element-butterflies of the pass's layers.
     chunk = 1 << (m - 1).bit_length()
     L_e = chunk.bit_length() - 1
@@ -452,11 +458,13 @@ def main():
     valu = None
     if layers is not None and L_e > 8:
         bfly = layers * (chunk // 2) * (S // 2)
-        peak = 1024 * 16 * 2.4e9 * 4 / 30
+        peak = 1024 * 256 / 115.7 * 2.4e9
         valu = {"bound": "valu", "kernel": dom, "achieved": round(bfly / dom_avg_s / 1e12, 3),
                 "peak": round(peak / 1e12, 3), "unit": "T element-butterflies/s", "frac": round(bfly / dom_avg_s / peak, 4),
                 "butterflies_per_launch": bfly,
-                "note": "ceiling of this kernel's multiply (30 VALU instructions per 4-element butterfly), not a vendor peak"}
+                "note": "measured issue ceiling of this kernel's butterfly (115.7 cycles per 30-instruction "
+                        "wave-quad-butterfly, profiles/r03_ubench_bfly.txt) at 2.4 GHz; the zero-twiddle groups "
+                        "the two-direction passes skip still count as butterflies here"}
 
     extra = {}
     if not args.no_extra and (k, m) != (1000, 1000):
