@@ -238,12 +238,25 @@ def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
     if world == 1:
         (comm,) = rs16.Comm.init_all([eng])
     else:
+        # unique id from rank 0 over the gloo control plane; the communicator
+        # init has a deadline (rs16_comm.cpp), and every rank learns whether
+        # all of them got one before any collective is issued
         import torch
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             uid[:] = torch.frombuffer(bytearray(rs16.Comm.unique_id()), dtype=torch.uint8)
         dist.broadcast(uid, 0)
-        comm = rs16.Comm(eng, world, rank, bytes(uid.numpy().tobytes()))
+        comm, why = None, ""
+        try:
+            comm = rs16.Comm(eng, world, rank, bytes(uid.numpy().tobytes()))
+        except Exception as exc:  # reported below, after every rank knows
+            why = f"{type(exc).__name__}: {exc}"
+        ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if comm is not None:
+                comm.close()
+            return {"error": f"RCCL communicator init failed on some rank ({why or 'another rank'})"}
     off, w = rs16.column_slice(S4, world, rank)
     root = rank == 0
     d_orig = d_rec = d_out = None
@@ -317,13 +330,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     dist = None
-    json_fd = None
+    # gloo and RCCL print connection / version banners on stdout: keep fd 1
+    # for the one JSON line of rank 0 and send everything else to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     if world > 1:
-        # gloo prints its connection messages on stdout: keep fd 1 for the
-        # one JSON line of rank 0 and send everything else to stderr
-        sys.stdout.flush()
-        json_fd = os.dup(1)
-        os.dup2(2, 1)
         import torch.distributed as dist  # control plane only (barrier, max of times)
         dist.init_process_group("gloo", init_method="env://")
 
@@ -621,10 +633,7 @@ def main():
             "extra": extra,
             "verified": verified,
         }
-        if json_fd is None:
-            print(json.dumps(out), flush=True)
-        else:
-            os.write(json_fd, (json.dumps(out) + "\n").encode())
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

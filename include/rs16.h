@@ -221,12 +221,20 @@ int rs16_encode_device(rs16_engine* eng, size_t original_count, size_t recovery_
  * shard of this kind was received", and the first pass then launches no
  * tile of that segment.  The counts MUST equal the number of nonzero flags
  * (a 0 count with set flags drops those shards and restores wrong data
- * without an error).  Lost originals are restored in place into
- * d_original.  Default rate selection as ReedSolomonDecoder. */
+ * without an error; rs16_decode_check detects it after the fact).  Lost
+ * originals are restored in place into d_original.  Default rate selection
+ * as ReedSolomonDecoder. */
 int rs16_decode_device(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
                        void* d_original, const uint8_t* d_original_received, const void* d_recovery,
                        const uint8_t* d_recovery_received, size_t original_received_count,
                        size_t recovery_received_count, void* stream, rs16_error* err);
+/* Checked mode of the engine's last decode: waits for `stream` and compares
+ * the received counts that decode was given with the rows the device flags
+ * mark received (the eval_poly kernels count them per 64-row chunk as they
+ * scan the flags, off the host's path).  RS16_OK when they agree (or no
+ * decode ran), else RS16_INVALID_ARGUMENT with v0 / v1 = the originals /
+ * recovery shards the flags mark received. */
+int rs16_decode_check(rs16_engine* eng, void* stream, rs16_error* err);
 /* Concurrent column slices of rs16_encode_device / rs16_decode_device (1..4,
  * default 1): the shard columns are split into slices of multiples of 64
  * bytes (each 64-byte column block is an independent codeword, so results

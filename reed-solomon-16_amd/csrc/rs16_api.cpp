@@ -106,6 +106,24 @@ extern "C" int rs16_engine_set_slices(rs16_engine* e, int n, rs16_error* err) {
     e->slices = n;
     return set_error(err, RS16_OK);
 }
+// The received counts of the engine's last decode against the device flags
+// (the eval_poly kernels count the received rows per 64-row chunk).
+extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) {
+    if (!e->last_dec_valid) return set_error(err, RS16_OK);
+    if (int rc = e->activate(err)) return rc;
+    RS16_HIP(hipStreamSynchronize(e->pick(stream)));
+    const DecodeGeom& g = e->last_dec;
+    const size_t chunks = ((size_t)g.n + 63) / 64;
+    std::vector<uint32_t> c(2 * chunks);
+    RS16_HIP(hipMemcpy(c.data(), e->ws_rcount.p, c.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t a = 0, b = 0;
+    for (size_t i = 0; i < chunks; i++) a += c[2 * i], b += c[2 * i + 1];
+    // (orig_recv, rec_recv) as the caller gave them to rs16_decode_device
+    const uint64_t want_o = g.high ? g.b_recv : g.a_recv, want_r = g.high ? g.a_recv : g.b_recv;
+    const uint64_t got_o = g.high ? b : a, got_r = g.high ? a : b;
+    if (got_o != want_o || got_r != want_r) return set_error(err, RS16_INVALID_ARGUMENT, got_o, got_r);
+    return set_error(err, RS16_OK);
+}
 extern "C" int rs16_set_diagnostics(int flags) {
     const int old = g_diag;
     g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL);
@@ -237,6 +255,7 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->ws_zflag.release();
     e->ws_rbits.release();
     e->ws_lost.release();
+    e->ws_rcount.release();
     for (auto& sl : e->hslot) {
         if (sl.s) (void)hipStreamSynchronize(sl.s), (void)hipStreamDestroy(sl.s);
         sl.orig.release(), sl.rec.release(), sl.z.release(), sl.u.release();
@@ -531,6 +550,9 @@ extern "C" const void* rs16_encoder_recovery_device(rs16_encoder* enc, size_t in
 }
 static const void* encoder_recovery_host(rs16_encoder* enc, size_t index, rs16_error* err) {
     if (!(enc->eng && enc->encoded && index < enc->m)) return set_error(err, RS16_OK), nullptr;
+    // (the common case -- rows already copied back -- makes no HIP call)
+    if (enc->out_on_host && !enc->out_done.busy)
+        return set_error(err, RS16_OK), (const uint8_t*)enc->h_out.p + index * enc->S;
     if (enc->eng->activate(err) || encoder_fetch(enc, err)) return nullptr;
     hipError_t he = enc->out_done.wait();
     if (he != hipSuccess) return hip_fail(err, he), nullptr;
@@ -789,6 +811,7 @@ extern "C" const void* rs16_decoder_restored_original_device(rs16_decoder* d, si
 }
 static const void* decoder_restored_host(rs16_decoder* d, size_t index, rs16_error* err) {
     if (!rs16_decoder_restored_original_device(d, index)) return set_error(err, RS16_OK), nullptr;
+    if (d->out_on_host && !d->out_done.busy) return set_error(err, RS16_OK), (const uint8_t*)d->h_out.p + index * d->S;
     if (d->eng->activate(err) || decoder_fetch(d, err)) return nullptr;
     hipError_t he = d->out_done.wait();
     if (he != hipSuccess) return hip_fail(err, he), nullptr;

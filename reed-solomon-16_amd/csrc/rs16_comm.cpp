@@ -16,8 +16,10 @@
 // communicators and issue them in one NCCL group.
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "rs16_engine.hpp"
@@ -28,6 +30,7 @@ struct rs16_comm {
     rs16_engine* eng = nullptr;
     ncclComm_t nc = nullptr;
     int nranks = 0, rank = 0;
+    bool blocking = false;  // ncclCommInitAll communicators are blocking
     DevBuf stage;  // root: packed column slices
 };
 
@@ -37,6 +40,27 @@ static int nccl_fail(rs16_error* err, ncclResult_t r) { return set_error(err, RS
         ncclResult_t _r = (call);                           \
         if (_r != ncclSuccess) return nccl_fail(err, _r);   \
     } while (0)
+
+// Communicators are non-blocking (ncclConfig_t::blocking = 0): init and
+// every group of sends / receives return at once and are waited for here
+// with a deadline, so a rank that never joins makes the others fail with an
+// error (the communicator aborted) instead of hanging the process.
+static constexpr double INIT_DEADLINE_S = 120.0, GROUP_DEADLINE_S = 60.0;
+static ncclResult_t settle(ncclComm_t c, ncclResult_t r, double deadline_s) {
+    if (r != ncclSuccess && r != ncclInProgress) return r;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        ncclResult_t q = ncclCommGetAsyncError(c, &st);
+        if (q != ncclSuccess) return q;
+        if (st != ncclInProgress) return st;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > deadline_s) {
+            (void)ncclCommAbort(c);
+            return ncclSystemError;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
 
 // Column slice of rank r of n (B = S / 64 blocks).
 static void col_slice(size_t S, int n, int r, size_t* off, size_t* w) {
@@ -61,8 +85,12 @@ extern "C" rs16_comm* rs16_comm_new(rs16_engine* eng, int nranks, int rank, cons
     if (!c) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
-    ncclResult_t r = ncclCommInitRank(&c->nc, nranks, u, rank);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&c->nc, nranks, u, rank, &cfg);
+    if (c->nc) r = settle(c->nc, r, INIT_DEADLINE_S);
     if (r != ncclSuccess) {
+        c->nc = nullptr;  // (aborted, or never created)
         delete c;
         return nccl_fail(err, r), nullptr;
     }
@@ -89,6 +117,7 @@ extern "C" int rs16_comm_init_all(rs16_engine* const* engines, int n, rs16_comm*
         comms[i]->nc = nc[i];
         comms[i]->nranks = n;
         comms[i]->rank = i;
+        comms[i]->blocking = true;
     }
     return set_error(err, RS16_OK);
 }
@@ -120,7 +149,7 @@ static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t
     const int nranks = comms[0]->nranks;
     if (root < 0 || root >= nranks) return set_error(err, RS16_INVALID_ARGUMENT);
     for (int i = 0; i < n; i++)
-        if (!comms[i] || comms[i]->nranks != nranks) return set_error(err, RS16_INVALID_ARGUMENT);
+        if (!comms[i] || !comms[i]->nc || comms[i]->nranks != nranks) return set_error(err, RS16_INVALID_ARGUMENT);
     auto strm = [&](rs16_comm* c) { return (n == 1 && stream) ? (hipStream_t)stream : c->eng->stream; };
     // root, scatter: pack the column slices (one pitched copy per rank)
     for (int i = 0; i < n; i++) {
@@ -169,7 +198,16 @@ static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t
             }
         }
     }
-    RS16_NCCL(ncclGroupEnd());
+    {
+        const ncclResult_t g = ncclGroupEnd();
+        for (int i = 0; i < n; i++) {
+            const ncclResult_t x = comms[i]->blocking ? g : settle(comms[i]->nc, g, GROUP_DEADLINE_S);
+            if (x != ncclSuccess) {
+                if (!comms[i]->blocking) comms[i]->nc = nullptr;  // (aborted by settle)
+                return nccl_fail(err, x);
+            }
+        }
+    }
     // root, gather: unpack into the full rows x S array
     if (!scatter)
         for (int i = 0; i < n; i++) {

@@ -318,6 +318,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     RS16_HIP(ws_zflag.reserve(256));
     RS16_HIP(ws_rbits.reserve(GF_ORDER / 8));
     RS16_HIP(ws_lost.reserve(256 * 8 + 16));
+    RS16_HIP(ws_rcount.reserve(GF_ORDER / 64 * 8));
     ErasureSpec es;
     es.flags_a = flags_a;
     es.flags_b = flags_b;
@@ -339,6 +340,9 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.lostpart = prune ? (uint32_t*)ws_lost.p : nullptr;
     es.lostrange = prune ? (uint32_t*)ws_lost.p + 512 : nullptr;
     es.orig_b = g.high ? 1 : 0;
+    es.rcount = (uint32_t*)ws_rcount.p;
+    last_dec = g;
+    last_dec_valid = true;
     es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;

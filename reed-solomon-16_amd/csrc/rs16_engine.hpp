@@ -81,6 +81,10 @@ struct rs16_engine {
     rs16::DevBuf ws_zflag;  // decode: per DEC_FIRST tile, 1 = no received row (tile skipped, rows zero)
     rs16::DevBuf ws_rbits;  // decode: received-row bitmap (65536 bits)
     rs16::DevBuf ws_lost;   // decode: lost-original row range per 256-row block (2 KiB) + overall (8 B)
+    rs16::DevBuf ws_rcount; // decode: received rows per 64-row chunk and segment (ErasureSpec::rcount)
+    // the last decode's geometry and the received counts it was given (rs16_decode_check)
+    rs16::DecodeGeom last_dec{};
+    bool last_dec_valid = false;
     // Host-resident pipeline (rs16_encode_host / rs16_decode_host): column
     // slices alternate between two slots, each with its own stream and the
     // device buffers of one slice, so copies and compute of different slices

@@ -162,6 +162,10 @@ struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.r
     uint32_t* lostpart;
     uint32_t* lostrange;
     uint32_t orig_b;
+    // Received rows per 64-row chunk of rows [0, n), by segment:
+    // rcount[2 c] = rows of segment A, rcount[2 c + 1] = rows of segment B
+    // (rs16_decode_check compares their sums with the caller's counts).
+    uint32_t* rcount;
     uint64_t* stamps;          // RS16_STAMPS builds: eval timeline (rs16_engine_set_stamps)
 };
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,

@@ -147,6 +147,15 @@ __device__ __forceinline__ void lost_range_wave(const ErasureSpec& e) {
         e.lostrange[1] = hi;
     }
 }
+// Received rows of the 64-row chunk at row r0 by segment (A = rows < a_count),
+// from the chunk's ballot: lane 0 writes rcount (ErasureSpec).
+__device__ __forceinline__ void chunk_counts(const ErasureSpec& e, uint32_t r0, uint64_t rcv, uint64_t rcv_a) {
+    if (e.rcount && (threadIdx.x & 63) == 0 && r0 < e.n) {
+        const uint32_t ca = (uint32_t)__popcll(rcv_a);
+        e.rcount[2 * (r0 >> 6)] = ca;
+        e.rcount[2 * (r0 >> 6) + 1] = (uint32_t)__popcll(rcv) - ca;
+    }
+}
 // Received-row bitmap and zero-tile flags of rows [base, base + 256) by one
 // wave, from the ballots rmask[j] of rows base + 64 j + lane: rbits words,
 // zflags per tile of 2^zlo rows.
@@ -255,6 +264,7 @@ __global__ void __launch_bounds__(64) fwht_lo_flags_kernel(ErasureSpec e, uint32
         const bool rcv = i < e.n && received_at(e, i);
         rmask[j] = __ballot(rcv);
         lmask[j] = __ballot(i < e.n && orig_row(e, i) && !rcv);
+        chunk_counts(e, base + 64u * j, rmask[j], __ballot(rcv && i < e.a_count));
     }
     block_flags_wave(e, base, rmask);
     if (e.lostpart) lost_part_wave(e, blockIdx.x, base, lmask);
@@ -393,7 +403,9 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t r = b0 + lane + 64u * i;
-            rmask[i] = __ballot(r < e.n && received_at(e, r));
+            const bool rcv = r < e.n && received_at(e, r);
+            rmask[i] = __ballot(rcv);
+            chunk_counts(e, b0 + 64u * i, rmask[i], __ballot(rcv && r < e.a_count));
         }
         block_flags_wave(e, b0, rmask);
     }
@@ -548,6 +560,7 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
             // workgroups j < NB: the pass metadata of block j (rows >= n
             // lie past both segments: never received)
             const uint64_t rb = __ballot(rcv);
+            chunk_counts(e, (uint32_t)hp * 256u + wv * 64u, rb, __ballot(rcv && in_a));
             if (lane == 0) {
                 words[2 * wv] = (uint32_t)rb;
                 words[2 * wv + 1] = (uint32_t)(rb >> 32);

@@ -612,13 +612,18 @@ def encode_device(original_count, recovery_count, shard_bytes, d_original, d_rec
 
 def decode_device(original_count, recovery_count, shard_bytes, d_original, d_original_received, d_recovery,
                   d_recovery_received, original_received_count, recovery_received_count, stream=None,
-                  engine: Optional[Engine] = None):
+                  engine: Optional[Engine] = None, check: bool = False):
+    """rs16_decode_device.  The received counts must equal the device flags'
+    counts; check=True waits for the decode and verifies that
+    (rs16_decode_check), raising InvalidArgument on a mismatch."""
     eng = engine or default_engine()
     err = RS16Error()
     _check(lib().rs16_decode_device(eng.h, original_count, recovery_count, shard_bytes, Engine._ptr(d_original),
                                     Engine._ptr(d_original_received), Engine._ptr(d_recovery),
                                     Engine._ptr(d_recovery_received), original_received_count,
                                     recovery_received_count, stream, C.byref(err)), err)
+    if check:
+        _check(lib().rs16_decode_check(eng.h, stream, C.byref(err)), err)
 
 
 def _host_ptr(x) -> int:

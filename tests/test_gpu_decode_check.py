@@ -1,0 +1,47 @@
+"""rs16_decode_check (include/rs16.h): the eval_poly kernels count the rows
+the device flags mark received, per 64-row chunk and segment, and the checked
+mode compares the sums with the counts the caller passed to
+rs16_decode_device (a count that disagrees with the flags
+restores wrong data; the reference derives its counts from its own received
+set, src/rate/decoder_work.rs:62-139, so it cannot disagree there).  Every
+eval_poly form is covered: one-kernel (block-aligned), two-kernel (unaligned
+flag arrays), the n <= 2048 form, the low rate."""
+import numpy as np
+import pytest
+
+import rs16
+from rs16.device import DeviceArray
+from rs16.util import generate_original
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("k,m,sb,unaligned", [(4096, 4096, 128, False), (4096, 4096, 128, True), (1000, 1000, 64, False),
+                                             (100, 300, 64, False), (3000, 60000, 64, False)])
+def test_counts_checked(k, m, sb, unaligned):
+    eng = rs16.default_engine()
+    orig = generate_original(k, sb, 9)
+    d_o, d_r = DeviceArray.from_numpy(eng, orig), DeviceArray(eng, m * sb)
+    rs16.encode_device(k, m, sb, d_o.ptr, d_r.ptr, engine=eng)
+    rng = np.random.default_rng(k)
+    lost = rng.choice(k, min(k, m) // 3 + 1, replace=False)
+    om = np.ones(k, np.uint8)
+    om[lost] = 0
+    rm = np.zeros(m, np.uint8)
+    rm[rng.choice(m, len(lost), replace=False)] = 1
+    pad = 1 if unaligned else 0
+    fo = np.concatenate([np.zeros(pad, np.uint8), om])
+    fr = np.concatenate([np.zeros(pad, np.uint8), rm])
+    d_fo, d_fr = DeviceArray.from_numpy(eng, fo), DeviceArray.from_numpy(eng, fr)
+    holes = orig.copy()
+    holes[lost] = 0
+    d_x = DeviceArray.from_numpy(eng, holes)
+    rs16.decode_device(k, m, sb, d_x.ptr, d_fo.ptr + pad, d_r.ptr, d_fr.ptr + pad, int(om.sum()), int(rm.sum()),
+                       engine=eng, check=True)
+    assert np.array_equal(d_x.download(shape=(k, sb)), orig)
+    # the same flags with a wrong original count: detected, with the flags' counts
+    d_x.upload(holes)
+    with pytest.raises(rs16.Error) as e:
+        rs16.decode_device(k, m, sb, d_x.ptr, d_fo.ptr + pad, d_r.ptr, d_fr.ptr + pad, int(om.sum()) - 1,
+                           int(rm.sum()) + 1, engine=eng, check=True)
+    assert e.value.kind == "InvalidArgument"
