@@ -227,8 +227,8 @@ def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
     recovery slices; then scatter the recovery, every rank decodes its slice
     at 100 % original loss, gather the restored originals.  Timed end to end
     (barrier + max over ranks) and as codec only / collectives only.  At one
-    rank the collectives are the root's pack / unpack copies and a send to
-    itself; the whole-stripe restore is checked on rank 0."""
+    rank the collectives are the root's own-slice copies (no RCCL traffic);
+    the whole-stripe restore is checked on rank 0."""
     import numpy as np
 
     import rs16

@@ -286,7 +286,8 @@ int rs16_decode_host_multi(rs16_engine* const* engines, int n, size_t original_c
  * array of shard_bytes = width, so every rank runs the device codec on its
  * slice with no further exchange -- and gathered back the same way.  The
  * root packs / unpacks with pitched device copies; the slices move with one
- * grouped ncclSend / ncclRecv per rank.  Ranks are processes (one
+ * grouped ncclSend / ncclRecv per other rank (the root's own slice is one
+ * pitched device copy, no RCCL).  Ranks are processes (one
  * rs16_comm_new each, with the root's rs16_comm_unique_id shared out of
  * band) or engines of one process (rs16_comm_init_all).  The collective
  * calls take this process's communicators (n of them, ranks in any order)

@@ -10,7 +10,8 @@
 // pitched device copy each into a staging buffer (rank r's slice = rows x w_r
 // contiguous bytes = a shard array of shard_bytes w_r), then one grouped
 // ncclSend / ncclRecv per rank moves them over xGMI.  The gather is the
-// mirror image.  Ranks may be processes (one rs16_comm each, ncclCommInitRank
+// mirror image.  The root's own slice never enters RCCL: one pitched device
+// copy between its full array and its slice.  Ranks may be processes (one rs16_comm each, ncclCommInitRank
 // with a shared unique id) or engines of one process (rs16_comm_init_all,
 // ncclCommInitAll); the collective calls take the array of this process's
 // communicators and issue them in one NCCL group.
@@ -151,21 +152,31 @@ static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t
     for (int i = 0; i < n; i++)
         if (!comms[i] || !comms[i]->nc || comms[i]->nranks != nranks) return set_error(err, RS16_INVALID_ARGUMENT);
     auto strm = [&](rs16_comm* c) { return (n == 1 && stream) ? (hipStream_t)stream : c->eng->stream; };
-    // root, scatter: pack the column slices (one pitched copy per rank)
+    // root: its own slice directly; scatter: pack the other ranks' slices
+    // (one pitched copy per rank)
     for (int i = 0; i < n; i++) {
         rs16_comm* c = comms[i];
         if (c->rank != root) continue;
         if (int rc = c->eng->activate(err)) return rc;
+        size_t off, w;
+        col_slice(S, nranks, root, &off, &w);
+        if (w && scatter)
+            RS16_HIP(hipMemcpy2DAsync(d_slice[i], w, (const uint8_t*)d_full[i] + off, S, w, rows,
+                                      hipMemcpyDeviceToDevice, strm(c)));
+        if (w && !scatter)
+            RS16_HIP(hipMemcpy2DAsync((uint8_t*)d_full[i] + off, S, d_slice[i], w, w, rows, hipMemcpyDeviceToDevice,
+                                      strm(c)));
+        if (nranks == 1) continue;
         RS16_HIP(c->stage.reserve(rows * S));
         if (scatter)
             for (int r = 0; r < nranks; r++) {
-                size_t off, w;
                 col_slice(S, nranks, r, &off, &w);
-                if (!w) continue;
+                if (!w || r == root) continue;
                 RS16_HIP(hipMemcpy2DAsync((uint8_t*)c->stage.p + rows * off, w, (const uint8_t*)d_full[i] + off, S, w,
                                           rows, hipMemcpyDeviceToDevice, strm(c)));
             }
     }
+    if (nranks == 1) return set_error(err, RS16_OK);
     RS16_NCCL(ncclGroupStart());
     for (int i = 0; i < n; i++) {
         rs16_comm* c = comms[i];
@@ -179,7 +190,7 @@ static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t
             for (int r = 0; r < nranks; r++) {
                 size_t o2, w2;
                 col_slice(S, nranks, r, &o2, &w2);
-                if (!w2) continue;
+                if (!w2 || r == root) continue;
                 uint8_t* p = (uint8_t*)c->stage.p + rows * o2;
                 ncclResult_t x = scatter ? ncclSend(p, rows * w2, ncclUint8, r, c->nc, strm(c))
                                          : ncclRecv(p, rows * w2, ncclUint8, r, c->nc, strm(c));
@@ -189,7 +200,7 @@ static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t
                 }
             }
         }
-        if (w) {
+        if (w && c->rank != root) {
             ncclResult_t x = scatter ? ncclRecv(d_slice[i], rows * w, ncclUint8, root, c->nc, strm(c))
                                      : ncclSend(d_slice[i], rows * w, ncclUint8, root, c->nc, strm(c));
             if (x != ncclSuccess) {
@@ -217,7 +228,7 @@ static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t
             for (int r = 0; r < nranks; r++) {
                 size_t off, w;
                 col_slice(S, nranks, r, &off, &w);
-                if (!w) continue;
+                if (!w || r == root) continue;
                 RS16_HIP(hipMemcpy2DAsync((uint8_t*)d_full[i] + off, S, (const uint8_t*)c->stage.p + rows * off, w, w,
                                           rows, hipMemcpyDeviceToDevice, strm(c)));
             }

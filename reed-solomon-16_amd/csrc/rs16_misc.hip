@@ -326,10 +326,36 @@ __device__ __forceinline__ int block_region(const ErasureSpec& e, uint32_t base)
     if (base - e.chunk < e.b_count) return 2;
     return 3;
 }
+// (RS16_EVAL_ABL, timing-only builds: 3 = an empty kernel)
+#ifndef RS16_EVAL_ABL
+#define RS16_EVAL_ABL 0
+#endif
+#ifndef RS16_STAMPS
+#define RS16_STAMPS 0
+#endif
+// (RS16_STAMPS builds: slots as rs16_pass.hip's stamp(), 0 start, 1 flags
+// in, 2 sums done, 10 store issued, 11 store done, 14 / 15 real time)
+__device__ __forceinline__ void estamp(const ErasureSpec& e, int i) {
+#if RS16_STAMPS
+    if (e.stamps && threadIdx.x == 0) {
+        e.stamps[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
+        if (i == 0) {
+            e.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+            e.stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            e.stamps[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        }
+        if (i == 11) e.stamps[blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+    }
+#else
+    (void)e;
+    (void)i;
+#endif
+}
 __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t* out32, const uint16_t* log_walsh) {
     __shared__ int xs[256];
     __shared__ uint32_t lr[2][4];
     const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    estamp(e, 0);
     uint32_t lw[4];
     if (wv == 0) {
 #pragma unroll
@@ -387,6 +413,7 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
             }
         }
     }
+    estamp(e, 1);
     xs[t] = (j == 0 ? 256 * all : 0) + (acc >> 7);
     if (j == 0 && e.lostrange) {
 #pragma unroll
@@ -415,6 +442,7 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
         e.lostrange[1] = max(max(lr[1][0], lr[1][1]), max(lr[1][2], lr[1][3]));
     }
     if (wv != 0) return;
+    estamp(e, 2);
     // ---- wave 0: y = H_hi(x) exactly, w = y * LW mod 65535, z = H_hi(w) ----
     int y[4];
 #pragma unroll
@@ -444,9 +472,15 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
         p = (p & 0xFFFFu) + (p >> 16);
         v[i] = (p & 0xFFFFu) + (p >> 16);
     }
+    estamp(e, 3);
     fwht256_wave(v);
+    estamp(e, 10);
 #pragma unroll
     for (int i = 0; i < 4; i++) out32[(lane + 64u * i) * 256u + j] = v[i];
+#if RS16_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    estamp(e, 11);
 }
 // Segment boundaries on 256-row blocks and 16-byte aligned flag arrays.
 static bool eval_fused_ok(const ErasureSpec& e) {
@@ -493,31 +527,6 @@ __device__ __forceinline__ uint32_t fold65535(uint32_t u) {
     return (u & 0xFFFFu) + (u >> 16);
 }
 __device__ __forceinline__ uint32_t mod65535(int v) { return fold65535((uint32_t)(v + 65535 * 4096)); }
-// (RS16_EVAL_ABL, timing-only builds: 3 = an empty kernel)
-#ifndef RS16_EVAL_ABL
-#define RS16_EVAL_ABL 0
-#endif
-#ifndef RS16_STAMPS
-#define RS16_STAMPS 0
-#endif
-// (RS16_STAMPS builds: slots as rs16_pass.hip's stamp(), 0 start, 1 flags
-// in, 2 sums done, 10 store issued, 11 store done, 14 / 15 real time)
-__device__ __forceinline__ void estamp(const ErasureSpec& e, int i) {
-#if RS16_STAMPS
-    if (e.stamps && threadIdx.x == 0) {
-        e.stamps[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
-        if (i == 0) {
-            e.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
-            e.stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            e.stamps[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-        }
-        if (i == 11) e.stamps[blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memrealtime();
-    }
-#else
-    (void)e;
-    (void)i;
-#endif
-}
 template <int NB>
 __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const uint16_t* log_walsh, uint32_t* z) {
     __shared__ int part[2][4][NB];  // per-wave parts of x and z

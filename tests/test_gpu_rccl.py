@@ -1,8 +1,8 @@
 """RCCL column-slice scatter / gather (include/rs16.h "RCCL over xGMI";
 SURVEY.md 8(e), BASELINE configs[4]) on the one GPU of the test box: a
 one-rank communicator (both ncclCommInitAll and ncclCommInitRank with a
-unique id), so the scatter and gather are the root's pack / unpack copies plus
-a grouped send / receive to itself.  More ranks need more GPUs; the partition
+unique id), so the scatter and gather are the root's own-slice copies (the
+root's slice never goes through RCCL).  More ranks need more GPUs; the partition
 rule they share is checked on CPU (tests/test_cabi.py), the multi-rank data
 flow with gloo (tests/test_distributed.py).  Here: the slices round-trip bit
 for bit, and encode + 100 %-loss decode through scatter -> device codec per
