@@ -526,6 +526,39 @@ def main():
                                      "received": f"originals 0..{k - L1}, recovery 0..{L1}"}
 
     if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
+        # The multi-chunk rate paths: high rate with k > chunk
+        # (60000:3000, 15 chunks of 4096) and low rate (3000:60000); encode,
+        # then a decode that loses min(k, m) originals (the last ones for the
+        # high rate, all of them for the low rate), restore checked.
+        rp = {}
+        for k3, m3 in ((60000, 3000), (3000, 60000)):
+            o3 = generate_original(k3, S, 3)
+            a3, r3 = DeviceArray.from_numpy(eng, o3), DeviceArray(eng, m3 * S)
+            lost3 = min(k3, m3)
+            of3 = np.ones(k3, np.uint8)
+            of3[k3 - lost3:] = 0
+            rf3 = np.zeros(m3, np.uint8)
+            rf3[:lost3] = 1
+            d_of3, d_rf3 = DeviceArray.from_numpy(eng, of3), DeviceArray.from_numpy(eng, rf3)
+            h3 = o3.copy()
+            h3[k3 - lost3:] = 0
+            x3 = DeviceArray.from_numpy(eng, h3)
+            e3 = lambda: rs16.encode_device(k3, m3, S, a3.ptr, r3.ptr, engine=eng)
+            d3 = lambda: rs16.decode_device(k3, m3, S, x3.ptr, d_of3.ptr, r3.ptr, d_rf3.ptr, k3 - lost3, lost3,
+                                            engine=eng)
+            e3()
+            d3()
+            assert np.array_equal(x3.download(shape=(k3, S)), o3), f"{k3}:{m3} decode did not restore"
+            n3 = max(5, args.steps // 2)
+            te3, td3 = timed(e3, n3), timed(d3, n3)
+            rp[f"{k3}:{m3}x{S}"] = {
+                "rate": "high" if rs16.use_high_rate(k3, m3) else "low",
+                "encode_gib_s": world * (k3 + m3) * S * n3 / te3 / GIB, "encode_us": te3 / n3 * 1e6,
+                "decode_gib_s": world * (k3 + m3) * S * n3 / td3 / GIB, "decode_us": td3 / n3 * 1e6,
+                "lost_originals": lost3}
+        extra["rate_paths"] = rp
+
+    if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
         extra["configs4_rccl"] = configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, args.steps)
 
     if not args.no_extra and world == 1:

@@ -534,9 +534,9 @@ extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
     if (enc->high && enc->k <= chunk)
         rc = e->encode_high_fused(enc->k, enc->m, enc->S, enc->S, w, w, w, e->stream, err);
     else if (enc->high)
-        rc = e->encode_high_generic(enc->k, enc->m, enc->S, w, enc->work_count, e->stream, err);
+        rc = e->encode_high_multi(enc->k, enc->m, enc->S, enc->S, w, w, w, e->stream, err);
     else
-        rc = e->encode_low_generic(enc->k, enc->m, enc->S, w, enc->work_count, e->stream, err);
+        rc = e->encode_low_multi(enc->k, enc->m, enc->S, enc->S, w, w, w, e->stream, err);
     if (rc) return rc;
     if (int rc2 = e->scratch_done(e->stream, err)) return rc2;
     // a host round gets its results back in one copy, right behind the passes
@@ -843,12 +843,8 @@ extern "C" int rs16_decoder_is_high_rate(const rs16_decoder* d) { return d->high
 static int encode_dev(rs16_engine* e, bool high, size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec,
                       uint8_t* Z, hipStream_t s, rs16_error* err) {
     if (high && k <= next_pow2(m)) return e->encode_high_fused(k, m, S, S, d_orig, d_rec, Z, s, err);
-    const size_t wc = rs16_encoder_work_count(high, k, m);
-    RS16_HIP(hipMemcpyAsync(Z, d_orig, k * S, hipMemcpyDeviceToDevice, s));
-    int rc = high ? e->encode_high_generic(k, m, S, Z, wc, s, err) : e->encode_low_generic(k, m, S, Z, wc, s, err);
-    if (rc) return rc;
-    RS16_HIP(hipMemcpyAsync(d_rec, Z, m * S, hipMemcpyDeviceToDevice, s));
-    return RS16_OK;
+    return high ? e->encode_high_multi(k, m, S, S, d_orig, d_rec, Z, s, err)
+                : e->encode_low_multi(k, m, S, S, d_orig, d_rec, Z, s, err);
 }
 
 extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, const void* d_original,

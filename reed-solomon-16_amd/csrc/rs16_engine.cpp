@@ -470,46 +470,94 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     return RS16_OK;
 }
 
-// HighRateEncoder::encode, general case (src/rate/rate_high.rs:44-83).
-int rs16_engine::encode_high_generic(size_t k, size_t m, size_t S, uint8_t* w, size_t work_count, hipStream_t s,
-                                     rs16_error* err) {
-    const size_t chunk = next_pow2(m);
-    const size_t first = std::min(k, chunk);
-    if (chunk > first) RS16_HIP(hipMemsetAsync(w + first * S, 0, (chunk - first) * S, s));
-    if (int rc = ifft(w, S, 0, chunk, chunk, s, err)) return rc;
-    if (k > chunk) {
-        size_t cs = chunk;
-        while (cs + chunk <= k) {
-            if (int rc = ifft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
-            RS16_HIP(launch_xor(w, w + cs * S, chunk * S, s));
-            cs += chunk;
-        }
-        const size_t last = k % chunk;
-        if (last > 0) {
-            RS16_HIP(hipMemsetAsync(w + (cs + last) * S, 0, (work_count - cs - last) * S, s));
-            if (int rc = ifft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
-            RS16_HIP(launch_xor(w, w + cs * S, chunk * S, s));
-        }
+// The FFT half of the multi-chunk encoders: FFT of nch chunks of Z (batched
+// like the IFFTs below, skew_delta applied to absolute rows), recovery rows
+// [0, m) stored to d_rec.
+int rs16_engine::fft_to_recovery(size_t m, size_t S, size_t S_user, uint8_t* Z, uint8_t* d_rec, size_t chunk,
+                                 uint32_t nch, uint32_t skew, hipStream_t s, rs16_error* err) {
+    const int L = ilog2(chunk), lo = L <= 8 ? L : L / 2, hi = L - lo;
+    PassArgs a = base_args(this, S);
+    a.skew_fft = skew;
+    if (hi) {
+        a.in = a.out = Z;
+        a.lo = lo;
+        RS16_PASS(GEN_FFT, hi, a, nch << lo, s);
     }
-    return fft(w, S, 0, chunk, 0, s, err);
+    a.in = Z;
+    a.out = d_rec;
+    a.S_out = S_user;
+    a.lo = 0;
+    a.out_rows = (uint32_t)m;
+    RS16_PASS(ENC_LAST, lo, a, (uint32_t)((m + ((size_t)1 << lo) - 1) >> lo), s);
+    return RS16_OK;
 }
 
-// LowRateEncoder::encode (src/rate/rate_low.rs:44-83).
-int rs16_engine::encode_low_generic(size_t k, size_t m, size_t S, uint8_t* w, size_t work_count, hipStream_t s,
-                                    rs16_error* err) {
-    (void)work_count;
+// HighRateEncoder::encode with more originals than one chunk
+// (src/rate/rate_high.rs:44-83): IFFT of every chunk c of the zero-padded
+// originals with skew_delta = c chunk + chunk (pos = c chunk), XOR of all of
+// them into chunk 0 (xor_within, :56-74), FFT of chunk 0 with skew 0.  The
+// twiddle of a layer at relative row r is skew[r + skew_delta + d - 1] =
+// skew[(c chunk + r) + chunk + d - 1]: the per-chunk transforms are one
+// transform over absolute rows with skew_delta = chunk whose layers stay
+// inside a chunk, so every chunk's IFFT runs in the same launches (tiles over
+// all chunks; the first pass gathers the originals, rows >= k read as zero),
+// then one XOR reduction, then the FFT.
+int rs16_engine::encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
+                                   uint8_t* Z, hipStream_t s, rs16_error* err) {
+    const size_t chunk = next_pow2(m);
+    const uint32_t nch = (uint32_t)((k + chunk - 1) / chunk);
+    const int L = ilog2(chunk), lo = L <= 8 ? L : L / 2, hi = L - lo;
+    if (L == 0) {  // one-row chunks: the single recovery row is the XOR of the originals
+        if (Z != d_orig) RS16_HIP(hipMemcpy2DAsync(Z, S, d_orig, S_user, S, k, hipMemcpyDeviceToDevice, s));
+        RS16_HIP(launch_xor_chunks(Z, S, nch, s));
+        if (d_rec != Z) RS16_HIP(hipMemcpyAsync(d_rec, Z, S, hipMemcpyDeviceToDevice, s));
+        return RS16_OK;
+    }
+    PassArgs a = base_args(this, S);
+    a.seg_a = d_orig;
+    a.S_seg = S_user;
+    a.a_count = (uint32_t)k;
+    a.skew_ifft = (uint32_t)chunk;
+    a.out = Z;
+    a.lo = 0;
+    RS16_PASS(ENC_FIRST, lo, a, nch << hi, s);
+    if (hi) {
+        a.in = a.out = Z;
+        a.lo = lo;
+        RS16_PASS(GEN_IFFT, hi, a, nch << lo, s);
+    }
+    RS16_HIP(launch_xor_chunks(Z, chunk * S, nch, s));
+    return fft_to_recovery(m, S, S_user, Z, d_rec, chunk, 1, 0, s, err);
+}
+
+// LowRateEncoder::encode (src/rate/rate_low.rs:44-83): IFFT of the
+// zero-padded originals (one chunk, skew 0), copied into every recovery chunk
+// c, FFT of each with skew_delta = c chunk + chunk -- batched as above
+// (absolute rows, skew_delta = chunk), recovery = rows [0, m).
+int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
+                                  uint8_t* Z, hipStream_t s, rs16_error* err) {
     const size_t chunk = next_pow2(k);
-    if (chunk > k) RS16_HIP(hipMemsetAsync(w + k * S, 0, (chunk - k) * S, s));
-    if (int rc = ifft(w, S, 0, chunk, 0, s, err)) return rc;
-    for (size_t cs = chunk; cs < m; cs += chunk)
-        RS16_HIP(hipMemcpyAsync(w + cs * S, w, chunk * S, hipMemcpyDeviceToDevice, s));
-    size_t cs = 0;
-    while (cs + chunk <= m) {
-        if (int rc = fft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
-        cs += chunk;
+    const uint32_t nch = (uint32_t)((m + chunk - 1) / chunk);
+    const int L = ilog2(chunk), lo = L <= 8 ? L : L / 2, hi = L - lo;
+    if (L == 0) {  // one original: every transform is the identity, every recovery row a copy
+        if (Z != d_orig) RS16_HIP(hipMemcpyAsync(Z, d_orig, S, hipMemcpyDeviceToDevice, s));
+        RS16_HIP(launch_copy_chunks(Z, S, nch, s));
+        if (d_rec != Z) RS16_HIP(hipMemcpy2DAsync(d_rec, S_user, Z, S, S, m, hipMemcpyDeviceToDevice, s));
+        return RS16_OK;
     }
-    if (m % chunk) {
-        if (int rc = fft(w, S, cs, chunk, cs + chunk, s, err)) return rc;
+    PassArgs a = base_args(this, S);
+    a.seg_a = d_orig;
+    a.S_seg = S_user;
+    a.a_count = (uint32_t)k;
+    a.skew_ifft = 0;
+    a.out = Z;
+    a.lo = 0;
+    RS16_PASS(ENC_FIRST, lo, a, 1u << hi, s);
+    if (hi) {
+        a.in = a.out = Z;
+        a.lo = lo;
+        RS16_PASS(GEN_IFFT, hi, a, 1u << lo, s);
     }
-    return RS16_OK;
+    RS16_HIP(launch_copy_chunks(Z, chunk * S, nch, s));
+    return fft_to_recovery(m, S, S_user, Z, d_rec, chunk, nch, (uint32_t)chunk, s, err);
 }

@@ -188,9 +188,14 @@ struct rs16_engine {
     // The half-transform decode applies (every original lost, originals
     // segment = one half of the work rows).
     static bool half_decode(const rs16::DecodeGeom& g);
-    // Generic (engine-op sequence) encoders, following the reference rate code.
-    int encode_high_generic(size_t k, size_t m, size_t S, uint8_t* work, size_t work_count, hipStream_t s,
-                            rs16_error* err);
-    int encode_low_generic(size_t k, size_t m, size_t S, uint8_t* work, size_t work_count, hipStream_t s,
-                           rs16_error* err);
+    // Multi-chunk encoders (high rate with k > chunk, low rate): every chunk's
+    // transform in one batched set of launches.  d_orig rows have pitch
+    // S_user, Z is the work space (work_count x S; may be d_orig), the
+    // recovery rows [0, m) go to d_rec (pitch S_user; may be Z).
+    int encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
+                          uint8_t* Z, hipStream_t s, rs16_error* err);
+    int encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
+                         uint8_t* Z, hipStream_t s, rs16_error* err);
+    int fft_to_recovery(size_t m, size_t S, size_t S_user, uint8_t* Z, uint8_t* d_rec, size_t chunk, uint32_t nch,
+                        uint32_t skew, hipStream_t s, rs16_error* err);
 };

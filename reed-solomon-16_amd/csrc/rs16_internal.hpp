@@ -139,6 +139,9 @@ hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, h
 // Elementwise / small kernels.
 hipError_t launch_mul(uint8_t* x, size_t bytes, uint32_t entry, const uint32_t* mul_tab, hipStream_t s);
 hipError_t launch_xor(uint8_t* x, const uint8_t* y, size_t bytes, hipStream_t s);
+// w[0, chunk_bytes) ^= the nch - 1 chunks behind it / chunk 0 copied into them
+hipError_t launch_xor_chunks(uint8_t* w, size_t chunk_bytes, uint32_t nch, hipStream_t s);
+hipError_t launch_copy_chunks(uint8_t* w, size_t chunk_bytes, uint32_t nch, hipStream_t s);
 hipError_t launch_formal_derivative(uint8_t* out, const uint8_t* in, size_t shard_count, size_t S, hipStream_t s);
 
 // FWHT / eval_poly.  `work` is a u32[65536] scratch.

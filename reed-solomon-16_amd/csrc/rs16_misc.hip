@@ -52,6 +52,41 @@ hipError_t launch_xor(uint8_t* x, const uint8_t* y, size_t bytes, hipStream_t s)
     return hipGetLastError();
 }
 
+// Multi-chunk encodes: w[0, cb) ^= XOR of the nch - 1 chunks behind it
+// (HighRateEncoder's xor_within accumulation, src/rate/rate_high.rs:56-74),
+// and chunk 0 copied into chunks 1 .. nch - 1 (LowRateEncoder's per-chunk
+// copy of the transformed originals, src/rate/rate_low.rs:56-74); 16 B per lane.
+__global__ void __launch_bounds__(256) xor_chunks_kernel(uint4* w, size_t c16, uint32_t nch) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < c16; i += (size_t)gridDim.x * blockDim.x) {
+        uint4 a = w[i];
+        for (uint32_t c = 1; c < nch; c++) {
+            const uint4 b = w[c * c16 + i];
+            a.x ^= b.x; a.y ^= b.y; a.z ^= b.z; a.w ^= b.w;
+        }
+        w[i] = a;
+    }
+}
+__global__ void __launch_bounds__(256) copy_chunks_kernel(uint4* w, size_t c16, uint32_t nch) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < c16; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 a = w[i];
+        for (uint32_t c = 1; c < nch; c++) w[c * c16 + i] = a;
+    }
+}
+hipError_t launch_xor_chunks(uint8_t* w, size_t chunk_bytes, uint32_t nch, hipStream_t s) {
+    const size_t c16 = chunk_bytes / 16;
+    if (!c16 || nch < 2) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>((c16 + 255) / 256, 8192);
+    hipLaunchKernelGGL(xor_chunks_kernel, dim3(grid), dim3(256), 0, s, (uint4*)w, c16, nch);
+    return hipGetLastError();
+}
+hipError_t launch_copy_chunks(uint8_t* w, size_t chunk_bytes, uint32_t nch, hipStream_t s) {
+    const size_t c16 = chunk_bytes / 16;
+    if (!c16 || nch < 2) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>((c16 + 255) / 256, 8192);
+    hipLaunchKernelGGL(copy_chunks_kernel, dim3(grid), dim3(256), 0, s, (uint4*)w, c16, nch);
+    return hipGetLastError();
+}
+
 // Engine::formal_derivative (src/engine.rs:233-238), closed form, out of place:
 // out[j] = in[j] ^ XOR_{b : j_b = 0, 2^b < n} in[j | 2^b]   (n a power of two).
 __global__ void __launch_bounds__(256) fd_kernel(uint4* out, const uint4* in, uint32_t n, size_t row16) {
