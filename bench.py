@@ -336,6 +336,11 @@ def main():
     json_fd = os.dup(1)
     os.dup2(2, 1)
     if world > 1:
+        # librs16.so first: its RCCL (ROCm's, the one include/rs16.h's
+        # rccl.h describes) must be the librccl.so.1 of this process, not the
+        # copy torch brings along (a different RCCL version)
+        from rs16._lib import lib as _rs16_lib
+        _rs16_lib()
         import torch.distributed as dist  # control plane only (barrier, max of times)
         dist.init_process_group("gloo", init_method="env://")
 

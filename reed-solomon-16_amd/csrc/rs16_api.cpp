@@ -2,6 +2,8 @@
 // encoder/decoder state machines (EncoderWork / DecoderWork semantics of
 // src/rate/{encoder,decoder}_work.rs) with HBM-resident work space, and the
 // device-resident one-shot codec.
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -46,7 +48,13 @@ extern "C" size_t rs16_error_message(const rs16_error* e, char* buf, size_t len)
     case RS16_UNSUPPORTED_SHARD_COUNT:
         snprintf(tmp, sizeof tmp, "unsupported shard count: %llu original shards with %llu recovery shards", a, b);
         break;
-    case RS16_DEVICE_ERROR: snprintf(tmp, sizeof tmp, "device error: %s", hipGetErrorString((hipError_t)a)); break;
+    case RS16_DEVICE_ERROR:
+        // v0 = hipError_t, or 1000 + ncclResult_t for an RCCL call (rs16_comm.cpp)
+        if (a >= 1000)
+            snprintf(tmp, sizeof tmp, "device error: RCCL: %s", ncclGetErrorString((ncclResult_t)(a - 1000)));
+        else
+            snprintf(tmp, sizeof tmp, "device error: %s", hipGetErrorString((hipError_t)a));
+        break;
     case RS16_INVALID_ARGUMENT: snprintf(tmp, sizeof tmp, "invalid argument"); break;
     default: snprintf(tmp, sizeof tmp, "unknown error %d", e->code); break;
     }

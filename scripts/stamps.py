@@ -37,13 +37,23 @@ def main():
     original = generate_original(k, S, 0)
     d_orig = DeviceArray.from_numpy(eng, original)
     d_rec = DeviceArray(eng, m * S)
-    d_rest = DeviceArray(eng, k * S)
-    d_of = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
-    d_rf = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+    # RS16_STAMPS_LOSS=L: the decode loses the last L originals and receives
+    # recovery 0..L (the reference bench's 1 % pattern for L = k / 100);
+    # default: every original lost (the half-transform decode)
+    L = int(os.environ.get("RS16_STAMPS_LOSS", k))
+    of = np.ones(k, np.uint8)
+    of[k - L:] = 0
+    rf = np.zeros(m, np.uint8)
+    rf[:L] = 1
+    held = original.copy()
+    held[k - L:] = 0
+    d_rest = DeviceArray.from_numpy(eng, held)
+    d_of = DeviceArray.from_numpy(eng, of)
+    d_rf = DeviceArray.from_numpy(eng, rf)
 
     def step():
         rs16.encode_device(k, m, S, d_orig.ptr, d_rec.ptr, engine=eng)
-        rs16.decode_device(k, m, S, d_rest.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, 0, m, engine=eng)
+        rs16.decode_device(k, m, S, d_rest.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, k - L, L, engine=eng)
 
     for _ in range(3):
         step()
