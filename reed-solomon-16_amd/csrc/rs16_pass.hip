@@ -201,6 +201,7 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
 //   -DRS16_ABLATE=3  as 1, and no table staging
 //   -DRS16_ABLATE=4  as 1, and no LDS exchanges / formal derivative
 //   -DRS16_ABLATE=5  loads / stores kept, but to L2-resident scratch (no HBM)
+//   -DRS16_ABLATE=7  butterflies kept, no LDS layout switches / formal derivative
 #ifndef RS16_ABLATE
 #define RS16_ABLATE 0
 #endif
@@ -629,7 +630,7 @@ template <int P, int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int P
 __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                        const PassArgs& a, const uint4* tab1, const uint4* tab2,
                                        uint32_t zmask = 0, const FIN& fin = FIN()) {
-    if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6)) {
+    if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6 || RS16_ABLATE == 7)) {
         uint32_t t0[20];
         load_table_lds(t0, group_table<T, LB, KB0, KB1, FFT, 0, IN_TAB2>(c, tab1, tab2));
         GroupLoop<P, T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0, FIN>::run(L, H, c, a, tab1, tab2, t0, zmask, fin);
@@ -734,7 +735,7 @@ template <int T, int NQR, bool FROM_B, class MID = NoMid>
 __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                          uint2* lds, MID mid = MID()) {
     constexpr int QL = Geo<T>::Q / NQR;
-    if (RS16_ABLATE == 4) return mid();
+    if (RS16_ABLATE == 4 || RS16_ABLATE == 7) return mid();
 #pragma unroll
     for (int r = 0; r < NQR; r++) {
         if (my_round<NQR>(c, r)) put_rows<T, QL, FROM_B>(L, H, c, lds);
@@ -762,7 +763,7 @@ __device__ __forceinline__ void tile_fd(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
                                         const uint32_t (&SL)[Geo<T>::NR], const uint32_t (&SH)[Geo<T>::NR],
                                         const Thr& c, uint2* lds) {
     constexpr int QL = Geo<T>::Q / NQR;
-    if (RS16_ABLATE == 4) return;
+    if (RS16_ABLATE == 4 || RS16_ABLATE == 7) return;
     if constexpr (T <= 4) {
         fd_rows<T, QL, LB>(L, H, SL, SH, c, lds);
     } else {
@@ -1139,7 +1140,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     // stores inside the last FFT block (one-item build, 16 rows per lane, not
     // the output-pruned DEC_MID; the reveal stores measured slower inside it)
     constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && P != DEC_MID && PT::STORE != ST_RESTORE &&
-                           (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6) && PT::FFT && T > 4;
+                           (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6 || RS16_ABLATE == 7) && PT::FFT && T > 4;
     uint2* lds = (uint2*)smem;
     const uint4* tab1 = (const uint4*)(smem + SM::TAB1_OFF);
     const uint4* tab2 = (const uint4*)(smem + SM::TAB2_OFF);
