@@ -506,6 +506,30 @@ def main():
         extra["1000:1000x1024"] = {"encode_gib_s": world * (k2 + m2) * S * n2 / te / GIB,
                                    "decode_gib_s": world * (k2 + m2) * S * n2 / td / GIB,
                                    "encode_us": te / n2 * 1e6, "decode_us": td / n2 * 1e6}
+        # Many such stripes per call (rs16_encode_device_batch; serving
+        # throughput, not the configs[1] latency): every stripe's recovery
+        # must equal the single-stripe encode above.
+        rec1 = r.download(shape=(m2, S))
+        bat = {}
+        for kb, nb in ((1000, 32), (100, 256)):
+            ob = o2[:kb] if kb <= k2 else generate_original(kb, S, seed)
+            db_o = DeviceArray.from_numpy(eng, np.tile(ob.reshape(1, -1), (nb, 1)))
+            db_r = DeviceArray(eng, nb * kb * S)
+            eb = lambda: rs16.encode_device_batch(kb, kb, S, nb, db_o.ptr, kb * S, db_r.ptr, kb * S, engine=eng)
+            eb()
+            got = db_r.download(shape=(nb, kb, S))
+            if kb == m2:
+                want = rec1
+            else:
+                d1o, d1r = DeviceArray.from_numpy(eng, ob), DeviceArray(eng, kb * S)
+                rs16.encode_device(kb, kb, S, d1o.ptr, d1r.ptr, engine=eng)
+                want = d1r.download(shape=(kb, S))
+            assert all(np.array_equal(got[i], want) for i in (0, nb // 2, nb - 1)), "batched encode differs"
+            tb = timed(eb, max(5, args.steps // 2))
+            nt = max(5, args.steps // 2)
+            bat[f"{kb}:{kb}x{S}x{nb}"] = {"encode_gib_s": world * nb * 2 * kb * S * nt / tb / GIB,
+                                          "us_per_call": tb / nt * 1e6, "stripes_per_call": nb}
+        extra["batched_stripes"] = bat
 
     if not args.no_extra and loss >= 100:
         # 1 % loss (benches/benchmarks.rs:84-87): originals 0..k-L and

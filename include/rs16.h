@@ -212,6 +212,20 @@ int rs16_decoder_is_high_rate(const rs16_decoder* dec);
  * recovery_count shards.  Default rate selection as ReedSolomonEncoder. */
 int rs16_encode_device(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
                        const void* d_original, void* d_recovery, void* stream, rs16_error* err);
+/* rs16_encode_device for `nstripes` independent stripes of one geometry in
+ * one call (many objects, each its own codeword set; SURVEY.md 8(f)3
+ * "batched independent codewords"): stripe i's original_count shards at
+ * d_original + i * original_stride bytes, its recovery_count shards written
+ * at d_recovery + i * recovery_stride (strides >= count * shard_bytes).
+ * Every stripe's result equals rs16_encode_device on it alone.  High-rate
+ * stripes with original_count <= next_pow2(recovery_count) -- every stripe
+ * with original_count <= recovery_count -- run batched, each pass launch
+ * covering all stripes, so stripes far below the chip's size (100:100,
+ * 1000:1000) still fill it; other shapes run stripe after stripe.  The
+ * reference encodes one stripe per call (src/lib.rs:242-279). */
+int rs16_encode_device_batch(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                             size_t nstripes, const void* d_original, size_t original_stride, void* d_recovery,
+                             size_t recovery_stride, void* stream, rs16_error* err);
 /* reed_solomon_16::decode (src/lib.rs:287-344), device-resident: d_original
  * holds original_count shard slots (received ones valid, flagged by the
  * device byte array d_original_received); d_recovery holds recovery_count

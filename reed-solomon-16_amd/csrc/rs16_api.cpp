@@ -887,6 +887,44 @@ extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     return set_error(err, RS16_OK);
 }
 
+// Many independent stripes of one geometry in one call: stripe i's originals
+// at d_original + i original_stride, its recovery at d_recovery + i
+// recovery_stride.  High-rate stripes with k <= chunk (every k <= m) run
+// batched -- each pass launch covers all stripes -- so small stripes fill the
+// chip; other shapes encode stripe by stripe.
+extern "C" int rs16_encode_device_batch(rs16_engine* e, size_t k, size_t m, size_t S, size_t nstripes,
+                                        const void* d_original, size_t original_stride, void* d_recovery,
+                                        size_t recovery_stride, void* stream, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    if (nstripes == 0) return set_error(err, RS16_OK);
+    if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S)
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    const size_t chunk = next_pow2(m);
+    // one launch holds < 2^32 tiles; stay far below
+    if (nstripes > ((size_t)1 << 20)) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
+    const size_t wc = rs16_encoder_work_count(high, k, m);
+    const uint8_t* o = (const uint8_t*)d_original;
+    uint8_t* r = (uint8_t*)d_recovery;
+    if (high && k <= chunk) {
+        RS16_HIP(e->ws_z.reserve(nstripes * chunk * S));
+        if (int rc = e->encode_high_fused(k, m, S, S, o, r, (uint8_t*)e->ws_z.p, s, err, nstripes, original_stride,
+                                          recovery_stride))
+            return rc;
+    } else {
+        RS16_HIP(e->ws_z.reserve(wc * S));
+        for (size_t i = 0; i < nstripes; i++)
+            if (int rc = encode_dev(e, high, k, m, S, o + i * original_stride, r + i * recovery_stride,
+                                    (uint8_t*)e->ws_z.p, s, err))
+                return rc;
+    }
+    if (int rc = e->scratch_done(s, err)) return rc;
+    return set_error(err, RS16_OK);
+}
+
 // ---------------------------------------------------------------------------
 // Host-resident one-shot codec: shards start and end in host memory.
 // ---------------------------------------------------------------------------

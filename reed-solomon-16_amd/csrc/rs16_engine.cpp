@@ -260,7 +260,7 @@ int rs16_engine::ifft(uint8_t* data, size_t S, size_t pos, size_t size, size_t s
 // as three passes over the 2-D row factorisation (contiguous low bits /
 // strided high bits); IFFT-high and FFT-high share the strided pass.
 int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
-                                   hipStream_t s, rs16_error* err) {
+                                   hipStream_t s, rs16_error* err, size_t nst, size_t bs_orig, size_t bs_rec) {
     const size_t chunk = next_pow2(m);
     const int L = ilog2(chunk);
     PassArgs a = base_args(this, S);
@@ -270,27 +270,39 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
     a.skew_ifft = (uint32_t)chunk;
     a.skew_fft = 0;
     a.out_rows = (uint32_t)m;
+    // nst > 1: independent stripes batched in each launch (PassArgs::stripe_tiles);
+    // stripe i's originals / recovery at d_orig / d_rec + i bs_orig / bs_rec,
+    // its work rows at Z + i chunk S
+    const uint32_t ns = (uint32_t)nst;
+    auto batch = [&](uint32_t tiles, size_t bs_in, size_t bs_out, size_t bs_seg) {
+        a.stripe_tiles = ns > 1 ? tiles : 0;
+        a.bs_in = bs_in;
+        a.bs_out = bs_out;
+        a.bs_seg = bs_seg;
+        return tiles * ns;
+    };
     if (L <= 8) {
         a.out = d_rec;
         a.S_out = S_user;
-        RS16_PASS(ENC_SINGLE, L, a, 1, s);
+        RS16_PASS(ENC_SINGLE, L, a, batch(1, 0, bs_rec, bs_orig), s);
         return RS16_OK;
     }
     // odd L: the extra row bit goes to the strided two-direction pass (an
     // 8 / 7 / 8 split measured 2-3 us slower per encode)
     const int lo = L / 2, hi = L - lo;
+    const size_t zs = chunk * S;
     a.out = Z;
     a.lo = 0;
-    RS16_PASS(ENC_FIRST, lo, a, 1u << hi, s);
+    RS16_PASS(ENC_FIRST, lo, a, batch(1u << hi, 0, zs, bs_orig), s);
     a.in = Z;
     a.lo = lo;
-    RS16_PASS(ENC_MID, hi, a, 1u << lo, s);
+    RS16_PASS(ENC_MID, hi, a, batch(1u << lo, zs, zs, 0), s);
     a.in = Z;
     a.out = d_rec;
     a.S_out = S_user;
     a.lo = 0;
     const uint32_t tiles = (uint32_t)((m + ((size_t)1 << lo) - 1) >> lo);
-    RS16_PASS(ENC_LAST, lo, a, tiles, s);
+    RS16_PASS(ENC_LAST, lo, a, batch(tiles, zs, bs_rec, 0), s);
     return RS16_OK;
 }
 

@@ -171,7 +171,7 @@ struct rs16_engine {
     // S = row width worked on (a column slice of the caller's arrays when
     // S < S_user), S_user = row stride of d_orig / d_rec (Z: stride S).
     int encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec, uint8_t* Z,
-                          hipStream_t s, rs16_error* err);
+                          hipStream_t s, rs16_error* err, size_t nstripes = 1, size_t bs_orig = 0, size_t bs_rec = 0);
     // Fused decode (both rates): seg_a / seg_b gather sources with device
     // flags; lost originals written to rest; Z, U work (n rows each; Z may
     // alias the sources when they live at their work positions).

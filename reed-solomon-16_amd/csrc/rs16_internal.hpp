@@ -118,6 +118,13 @@ struct PassArgs {
     const uint32_t* lostrange;
     // diagnostic timeline buffer (RS16_STAMPS builds; nullptr otherwise)
     uint64_t* stamps;
+    // Independent stripes in one launch (rs16_encode_device_batch): tiles
+    // [s * stripe_tiles, (s + 1) * stripe_tiles) belong to stripe s, which
+    // reads / writes in, out and seg_a displaced by s * bs_in / bs_out /
+    // bs_seg bytes; its twiddles are those of tile (tile - s * stripe_tiles).
+    // stripe_tiles == 0: one stripe.
+    uint32_t stripe_tiles;
+    uint64_t bs_in, bs_out, bs_seg;
 };
 
 // Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):

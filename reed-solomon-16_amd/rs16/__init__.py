@@ -26,7 +26,7 @@ from ._lib import RS16Error, lib
 __all__ = [
     "Error", "Engine", "default_engine", "ReedSolomonEncoder", "ReedSolomonDecoder", "RateEncoder",
     "RateDecoder", "EncoderResult", "DecoderResult", "encode", "decode", "encode_device", "decode_device",
-    "supports", "validate", "use_high_rate", "encoder_work_count", "decoder_work_count",
+    "supports", "validate", "use_high_rate", "encode_device_batch", "encoder_work_count", "decoder_work_count",
     "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS", "set_diagnostics",
     "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL", "encode_host", "decode_host",
     "encode_host_multi", "decode_host_multi", "Comm", "column_slice", "scatter_columns", "gather_columns",
@@ -608,6 +608,17 @@ def encode_device(original_count, recovery_count, shard_bytes, d_original, d_rec
     err = RS16Error()
     _check(lib().rs16_encode_device(eng.h, original_count, recovery_count, shard_bytes, Engine._ptr(d_original),
                                     Engine._ptr(d_recovery), stream, C.byref(err)), err)
+
+
+def encode_device_batch(original_count, recovery_count, shard_bytes, nstripes, d_original, original_stride,
+                        d_recovery, recovery_stride, stream=None, engine: Optional[Engine] = None):
+    """rs16_encode_device_batch: nstripes independent stripes, stripe i at
+    d_original + i * original_stride / d_recovery + i * recovery_stride (bytes)."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_encode_device_batch(eng.h, original_count, recovery_count, shard_bytes, nstripes,
+                                          Engine._ptr(d_original), original_stride, Engine._ptr(d_recovery),
+                                          recovery_stride, stream, C.byref(err)), err)
 
 
 def decode_device(original_count, recovery_count, shard_bytes, d_original, d_original_received, d_recovery,
