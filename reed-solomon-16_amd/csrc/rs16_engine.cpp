@@ -485,17 +485,22 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
 // The FFT half of the multi-chunk encoders: FFT of nch chunks of Z (batched
 // like the IFFTs below, skew_delta applied to absolute rows), recovery rows
 // [0, m) stored to d_rec.
-int rs16_engine::fft_to_recovery(size_t m, size_t S, size_t S_user, uint8_t* Z, uint8_t* d_rec, size_t chunk,
-                                 uint32_t nch, uint32_t skew, hipStream_t s, rs16_error* err) {
+int rs16_engine::fft_to_recovery(size_t m, size_t S, size_t S_user, const uint8_t* src, uint8_t* Z, uint8_t* d_rec,
+                                 size_t chunk, uint32_t nch, uint32_t skew, hipStream_t s, rs16_error* err) {
     const int L = ilog2(chunk), lo = L <= 8 ? L : L / 2, hi = L - lo;
     PassArgs a = base_args(this, S);
     a.skew_fft = skew;
+    // src != Z: every chunk's FFT reads the one chunk at src (the first pass only)
+    const uint32_t mask = src != Z ? (uint32_t)(chunk - 1) : 0u;
+    a.in = src;
+    a.in_rows_mask = mask;
     if (hi) {
-        a.in = a.out = Z;
+        a.out = Z;
         a.lo = lo;
         RS16_PASS(GEN_FFT, hi, a, nch << lo, s);
+        a.in = Z;
+        a.in_rows_mask = 0;
     }
-    a.in = Z;
     a.out = d_rec;
     a.S_out = S_user;
     a.lo = 0;
@@ -539,13 +544,15 @@ int rs16_engine::encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, 
         RS16_PASS(GEN_IFFT, hi, a, nch << lo, s);
     }
     RS16_HIP(launch_xor_chunks(Z, chunk * S, nch, s));
-    return fft_to_recovery(m, S, S_user, Z, d_rec, chunk, 1, 0, s, err);
+    return fft_to_recovery(m, S, S_user, Z, Z, d_rec, chunk, 1, 0, s, err);
 }
 
 // LowRateEncoder::encode (src/rate/rate_low.rs:44-83): IFFT of the
 // zero-padded originals (one chunk, skew 0), copied into every recovery chunk
 // c, FFT of each with skew_delta = c chunk + chunk -- batched as above
-// (absolute rows, skew_delta = chunk), recovery = rows [0, m).
+// (absolute rows, skew_delta = chunk), recovery = rows [0, m).  The copies
+// are not made: the transformed chunk goes to the scratch U and the FFT's
+// first pass reads it for every chunk (PassArgs::in_rows_mask).
 int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
                                   uint8_t* Z, hipStream_t s, rs16_error* err) {
     const size_t chunk = next_pow2(k);
@@ -557,19 +564,20 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
         if (d_rec != Z) RS16_HIP(hipMemcpy2DAsync(d_rec, S_user, Z, S, S, m, hipMemcpyDeviceToDevice, s));
         return RS16_OK;
     }
+    RS16_HIP(ws_u.reserve(chunk * S));
+    uint8_t* U = (uint8_t*)ws_u.p;
     PassArgs a = base_args(this, S);
     a.seg_a = d_orig;
     a.S_seg = S_user;
     a.a_count = (uint32_t)k;
     a.skew_ifft = 0;
-    a.out = Z;
+    a.out = U;
     a.lo = 0;
     RS16_PASS(ENC_FIRST, lo, a, 1u << hi, s);
     if (hi) {
-        a.in = a.out = Z;
+        a.in = a.out = U;
         a.lo = lo;
         RS16_PASS(GEN_IFFT, hi, a, 1u << lo, s);
     }
-    RS16_HIP(launch_copy_chunks(Z, chunk * S, nch, s));
-    return fft_to_recovery(m, S, S_user, Z, d_rec, chunk, nch, (uint32_t)chunk, s, err);
+    return fft_to_recovery(m, S, S_user, U, Z, d_rec, chunk, nch, (uint32_t)chunk, s, err);
 }

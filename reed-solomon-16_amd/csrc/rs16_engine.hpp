@@ -196,6 +196,6 @@ struct rs16_engine {
                           uint8_t* Z, hipStream_t s, rs16_error* err);
     int encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
                          uint8_t* Z, hipStream_t s, rs16_error* err);
-    int fft_to_recovery(size_t m, size_t S, size_t S_user, uint8_t* Z, uint8_t* d_rec, size_t chunk, uint32_t nch,
-                        uint32_t skew, hipStream_t s, rs16_error* err);
+    int fft_to_recovery(size_t m, size_t S, size_t S_user, const uint8_t* src, uint8_t* Z, uint8_t* d_rec,
+                        size_t chunk, uint32_t nch, uint32_t skew, hipStream_t s, rs16_error* err);
 };

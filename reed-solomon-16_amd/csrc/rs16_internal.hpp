@@ -125,6 +125,10 @@ struct PassArgs {
     // stripe_tiles == 0: one stripe.
     uint32_t stripe_tiles;
     uint64_t bs_in, bs_out, bs_seg;
+    // Plain loads read row (r & in_rows_mask) of `in` (0: row r): the low-rate
+    // encoder's FFTs of every recovery chunk read the one transformed chunk
+    // of originals instead of copies of it.
+    uint32_t in_rows_mask;
 };
 
 // Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):

@@ -829,7 +829,8 @@ __device__ __forceinline__ void load_rows(const PassArgs& a, const Thr& c, uint3
         const LaneOff<V32> lo(lr, a.S_in, c.offL);
 #pragma unroll
         for (int m = 0; m < NR; m++) {
-            const uint32_t ur = wr(m);
+            // (in_rows_mask: every chunk of the launch reads the one chunk at in)
+            const uint32_t ur = a.in_rows_mask ? (wr(m) & a.in_rows_mask) : wr(m);
             ld_sel(a, lo.at(sgpr_ptr(a.in + (uint64_t)ur * a.S_in)), c.active & !((d.zrow >> m) & 1u), c.offL, d.L[m], d.H[m]);
         }
     } else if constexpr (PT::LOAD == LD_GATHER_ENC) {
