@@ -525,10 +525,23 @@ def main():
                 rs16.encode_device(kb, kb, S, d1o.ptr, d1r.ptr, engine=eng)
                 want = d1r.download(shape=(kb, S))
             assert all(np.array_equal(got[i], want) for i in (0, nb // 2, nb - 1)), "batched encode differs"
-            tb = timed(eb, max(5, args.steps // 2))
             nt = max(5, args.steps // 2)
+            tb = timed(eb, nt)
+            # the same stripes decoded at 100 % original loss with one shared
+            # pattern (rs16_decode_device_batch: a failed device), restore checked
+            fo = DeviceArray.from_numpy(eng, np.zeros(kb, np.uint8))
+            fr = DeviceArray.from_numpy(eng, np.ones(kb, np.uint8))
+            dx = DeviceArray.from_numpy(eng, np.zeros(nb * kb * S, np.uint8))
+            dbf = lambda: rs16.decode_device_batch(kb, kb, S, nb, dx.ptr, kb * S, fo.ptr, db_r.ptr, kb * S, fr.ptr,
+                                                   0, kb, engine=eng)
+            dbf()
+            back = dx.download(shape=(nb, kb, S))
+            assert all(np.array_equal(back[i], ob) for i in (0, nb // 2, nb - 1)), "batched decode did not restore"
+            td = timed(dbf, nt)
             bat[f"{kb}:{kb}x{S}x{nb}"] = {"encode_gib_s": world * nb * 2 * kb * S * nt / tb / GIB,
-                                          "us_per_call": tb / nt * 1e6, "stripes_per_call": nb}
+                                          "encode_us_per_call": tb / nt * 1e6,
+                                          "decode_100pct_gib_s": world * nb * 2 * kb * S * nt / td / GIB,
+                                          "decode_us_per_call": td / nt * 1e6, "stripes_per_call": nb}
         extra["batched_stripes"] = bat
 
     if not args.no_extra and loss >= 100:

@@ -242,6 +242,18 @@ int rs16_decode_device(rs16_engine* eng, size_t original_count, size_t recovery_
                        void* d_original, const uint8_t* d_original_received, const void* d_recovery,
                        const uint8_t* d_recovery_received, size_t original_received_count,
                        size_t recovery_received_count, void* stream, rs16_error* err);
+/* rs16_decode_device for `nstripes` independent stripes that lost the same
+ * shards -- the case of a failed device, which holds the same shard index of
+ * every stripe: the received flags and counts are shared, stripe i's
+ * original slots at d_original + i * original_stride bytes (lost ones
+ * restored in place), its recovery at d_recovery + i * recovery_stride.
+ * One eval_poly for all, every pass launch covering all stripes.  Every
+ * stripe's result equals rs16_decode_device on it alone. */
+int rs16_decode_device_batch(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                             size_t nstripes, void* d_original, size_t original_stride,
+                             const uint8_t* d_original_received, const void* d_recovery, size_t recovery_stride,
+                             const uint8_t* d_recovery_received, size_t original_received_count,
+                             size_t recovery_received_count, void* stream, rs16_error* err);
 /* Checked mode of the engine's last decode: waits for `stream` and compares
  * the received counts that decode was given with the rows the device flags
  * mark received (the eval_poly kernels count them per 64-row chunk as they

@@ -1186,6 +1186,47 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     return set_error(err, RS16_OK);
 }
 
+// rs16_decode_device for nstripes independent stripes that lost the same
+// shards (one failed device holds the same shard index of every stripe):
+// one eval_poly from the shared flags, every pass launch covering all
+// stripes; stripe i's originals at d_original + i original_stride (restored
+// in place), its recovery at d_recovery + i recovery_stride.
+extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size_t S, size_t nstripes,
+                                        void* d_original, size_t original_stride, const uint8_t* d_original_received,
+                                        const void* d_recovery, size_t recovery_stride,
+                                        const uint8_t* d_recovery_received, size_t orig_recv, size_t rec_recv,
+                                        void* stream, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
+    if (nstripes == 0 || orig_recv == k) return set_error(err, RS16_OK);
+    if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S ||
+        nstripes > ((size_t)1 << 20))
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
+    DecodeGeom g = decode_geom(high, k, m);
+    g.a_recv = high ? rec_recv : orig_recv;
+    g.b_recv = high ? orig_recv : rec_recv;
+    RS16_HIP(e->ws_z.reserve(nstripes * g.n * S));
+    RS16_HIP(e->ws_u.reserve(nstripes * g.n * S));
+    const uint8_t* orig = (const uint8_t*)d_original;
+    const uint8_t* rec = (const uint8_t*)d_recovery;
+    const uint8_t* seg_a = high ? rec : orig;
+    const uint8_t* seg_b = high ? orig : rec;
+    const size_t bs_a = high ? recovery_stride : original_stride, bs_b = high ? original_stride : recovery_stride;
+    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
+    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
+    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err)) return rc;
+    if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
+                                  (uint8_t*)e->ws_u.p, s, err, nstripes, bs_a, bs_b, original_stride))
+        return rc;
+    if (int rc = e->scratch_done(s, err)) return rc;
+    return set_error(err, RS16_OK);
+}
+
 // ---------------------------------------------------------------------------
 // Device memory helpers.
 // ---------------------------------------------------------------------------

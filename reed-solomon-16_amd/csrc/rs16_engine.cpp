@@ -396,7 +396,7 @@ bool rs16_engine::half_decode(const DecodeGeom& g) {
 // ws_work32 (erasure logs), ws_rbits (received rows) and ws_zflag (zero tiles).
 int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                                const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
-                               hipStream_t s, rs16_error* err) {
+                               hipStream_t s, rs16_error* err, size_t nst, size_t bs_a, size_t bs_b, size_t bs_rest) {
     PassArgs a = base_args(this, S);
     a.S_seg = a.S_rest = S_user;
     a.seg_a = seg_a;
@@ -412,6 +412,22 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.rest_seg_b = g.high ? 1 : 0;
     a.rbits = (const uint32_t*)ws_rbits.p;
     a.skew_ifft = a.skew_fft = 0;
+    // nst > 1: independent stripes with one erasure pattern (rs16_decode_device_batch):
+    // every launch covers all of them (PassArgs::stripe_tiles); stripe i's
+    // segments / restored originals at + i bs_a / bs_b / bs_rest, its work
+    // rows at Z / U + i n S
+    const uint32_t ns = (uint32_t)nst;
+    const size_t zs = (size_t)g.n * S;
+    a.bs_seg = bs_a;
+    a.bs_seg_b = bs_b;
+    a.bs_rest = bs_rest;
+    auto batch = [&](uint32_t tiles, size_t bs_in, size_t bs_in2, size_t bs_out) {
+        a.stripe_tiles = ns > 1 ? tiles : 0;
+        a.bs_in = bs_in;
+        a.bs_in2 = bs_in2;
+        a.bs_out = bs_out;
+        return tiles * ns;
+    };
     const int L = ilog2(g.n);
     if (half_decode(g)) {
         const uint32_t half = g.n / 2, src = g.high ? 0 : half, dst = g.high ? half : 0;
@@ -421,23 +437,23 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         const int Lh = L - 1;
         if (Lh <= 8) {
             a.ework = nullptr;  // (decode_eval did the whole eval_poly)
-            RS16_PASS(DEC_HALF_SINGLE, Lh, a, 1, s);
+            RS16_PASS(DEC_HALF_SINGLE, Lh, a, batch(1, 0, 0, 0), s);
             return RS16_OK;
         }
         const int lo = Lh / 2, hi = Lh - lo;
         a.lo = 0;
         a.out = Z;
-        RS16_PASS_AS(PROF_DEC_HALF_FIRST, DEC_FIRST, lo, a, 1u << hi, s);
+        RS16_PASS_AS(PROF_DEC_HALF_FIRST, DEC_FIRST, lo, a, batch(1u << hi, 0, 0, zs), s);
         a.lo = lo;
         a.in = Z;
-        RS16_PASS_AS(PROF_DEC_HALF_MID, ENC_MID, hi, a, 1u << lo, s);
+        RS16_PASS_AS(PROF_DEC_HALF_MID, ENC_MID, hi, a, batch(1u << lo, zs, 0, zs), s);
         a.lo = 0;
         a.out = nullptr;
-        RS16_PASS(DEC_HALF_LAST, lo, a, (orig + (1u << lo) - 1) >> lo, s);
+        RS16_PASS(DEC_HALF_LAST, lo, a, batch((orig + (1u << lo) - 1) >> lo, zs, 0, 0), s);
         return RS16_OK;
     }
     if (L <= 8) {
-        RS16_PASS(DEC_SINGLE, L, a, 1, s);
+        RS16_PASS(DEC_SINGLE, L, a, batch(1, 0, 0, 0), s);
         return RS16_OK;
     }
     const int lo = L / 2, hi = L - lo;
@@ -458,7 +474,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.tile_base = t0z;
     a.lo = 0;
     a.out = Z;
-    RS16_PASS(DEC_FIRST, lo, a, t1z - t0z, s);
+    RS16_PASS(DEC_FIRST, lo, a, batch(t1z - t0z, 0, 0, zs), s);
     a.tile_base = 0;
     // Only tiles that contain original rows are needed in the last pass,
     // so DEC_MID computes and stores only U rows of those tiles (its tile
@@ -471,14 +487,14 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.out = U;
     a.need_lo = t0;
     a.need_hi = t1;
-    RS16_PASS(DEC_MID, hi, a, 1u << lo, s);
+    RS16_PASS(DEC_MID, hi, a, batch(1u << lo, zs, 0, zs), s);
     a.need_lo = a.need_hi = 0;
     a.lo = 0;
     a.in = Z;
     a.in2 = U;
     a.out = nullptr;
     a.tile_base = t0;
-    RS16_PASS(DEC_LAST, lo, a, t1 - t0, s);
+    RS16_PASS(DEC_LAST, lo, a, batch(t1 - t0, zs, zs, 0), s);
     return RS16_OK;
 }
 

@@ -184,7 +184,8 @@ struct rs16_engine {
                     rs16_error* err);
     int decode_passes(const rs16::DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                       const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
-                      hipStream_t s, rs16_error* err);
+                      hipStream_t s, rs16_error* err, size_t nstripes = 1, size_t bs_a = 0, size_t bs_b = 0,
+                      size_t bs_rest = 0);
     // The half-transform decode applies (every original lost, originals
     // segment = one half of the work rows).
     static bool half_decode(const rs16::DecodeGeom& g);

@@ -118,13 +118,15 @@ struct PassArgs {
     const uint32_t* lostrange;
     // diagnostic timeline buffer (RS16_STAMPS builds; nullptr otherwise)
     uint64_t* stamps;
-    // Independent stripes in one launch (rs16_encode_device_batch): tiles
-    // [s * stripe_tiles, (s + 1) * stripe_tiles) belong to stripe s, which
-    // reads / writes in, out and seg_a displaced by s * bs_in / bs_out /
-    // bs_seg bytes; its twiddles are those of tile (tile - s * stripe_tiles).
-    // stripe_tiles == 0: one stripe.
+    // Independent stripes in one launch (rs16_encode_device_batch,
+    // rs16_decode_device_batch): tiles [s * stripe_tiles, (s + 1) *
+    // stripe_tiles) belong to stripe s, which reads / writes in, in2, out,
+    // seg_a, seg_b and rest displaced by s times bs_in, bs_in2, bs_out,
+    // bs_seg, bs_seg_b, bs_rest bytes; its twiddles and decode metadata are
+    // those of tile (tile - s * stripe_tiles) (+ tile_base).  stripe_tiles ==
+    // 0: one stripe.
     uint32_t stripe_tiles;
-    uint64_t bs_in, bs_out, bs_seg;
+    uint64_t bs_in, bs_out, bs_seg, bs_in2, bs_seg_b, bs_rest;
     // Plain loads read row (r & in_rows_mask) of `in` (0: row r): the low-rate
     // encoder's FFTs of every recovery chunk read the one transformed chunk
     // of originals instead of copies of it.

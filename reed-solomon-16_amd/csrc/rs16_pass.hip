@@ -60,10 +60,6 @@ enum StoreMode { ST_PLAIN = 0, ST_RECOVERY, ST_RESTORE };
 // plain stores in the two-direction passes (same-box A/B, DESIGN.md 6.1:
 // nt / sc1 / sc0 sc1 everywhere and nt loads all measured slower).
 template <int P> struct ProgTraits;
-// decode programs (their tiles carry decode metadata; never batched)
-template <int P>
-constexpr bool PT_DECODE = P == DEC_FIRST || P == DEC_MID || P == DEC_LAST || P == DEC_SINGLE ||
-                           P == DEC_HALF_LAST || P == DEC_HALF_SINGLE;
 #define RS16_PROG(P, LD, I, F, FF, ST)          \
     template <> struct ProgTraits<P> {         \
         static constexpr int LOAD = LD;        \
@@ -807,9 +803,6 @@ __device__ __forceinline__ void set_item(Thr& c, const PassArgs& a, uint32_t ite
         tile = item / a.nslab;
         slab = item - tile * a.nslab;
     }
-    tile += a.tile_base;
-    c.b_low = tile & ((1u << a.lo) - 1);
-    c.b_high = tile >> a.lo;
     const uint32_t Qg = slab * Q + c.qt;
     c.active = Qg < a.qrow;
     c.offL = (Qg >> 3) * 64 + (Qg & 7) * 4;
@@ -1299,18 +1292,20 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
 
     uint32_t tile, slab;
     set_item(c, a, item, G::Q, tile, slab);
-    if constexpr (!PT_DECODE<P>) {
-        if (a.stripe_tiles) {
-            // batched stripes (encode programs): the stripe's arrays, its tile
-            const uint32_t st = uni(tile / a.stripe_tiles);
-            tile -= st * a.stripe_tiles;
-            c.b_low = tile & ((1u << a.lo) - 1);
-            c.b_high = tile >> a.lo;
-            a.in += st * a.bs_in;
-            a.out += st * a.bs_out;
-            a.seg_a += st * a.bs_seg;
-        }
+    if (a.stripe_tiles) {
+        // batched stripes: the stripe's arrays, the tile within the stripe
+        const uint32_t st = uni(tile / a.stripe_tiles);
+        tile -= st * a.stripe_tiles;
+        a.in += st * a.bs_in;
+        a.in2 += st * a.bs_in2;
+        a.out += st * a.bs_out;
+        a.seg_a += st * a.bs_seg;
+        a.seg_b += st * a.bs_seg_b;
+        a.rest += st * a.bs_rest;
     }
+    tile += a.tile_base;
+    c.b_low = tile & ((1u << a.lo) - 1);
+    c.b_high = tile >> a.lo;
     if constexpr (P == DEC_FIRST) {
         // a tile without received rows is skipped (process_item): return
         // before its table staging and row loads, so its slot frees at once

@@ -26,7 +26,7 @@ from ._lib import RS16Error, lib
 __all__ = [
     "Error", "Engine", "default_engine", "ReedSolomonEncoder", "ReedSolomonDecoder", "RateEncoder",
     "RateDecoder", "EncoderResult", "DecoderResult", "encode", "decode", "encode_device", "decode_device",
-    "supports", "validate", "use_high_rate", "encode_device_batch", "encoder_work_count", "decoder_work_count",
+    "supports", "validate", "use_high_rate", "encode_device_batch", "decode_device_batch", "encoder_work_count", "decoder_work_count",
     "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS", "set_diagnostics",
     "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL", "encode_host", "decode_host",
     "encode_host_multi", "decode_host_multi", "Comm", "column_slice", "scatter_columns", "gather_columns",
@@ -619,6 +619,19 @@ def encode_device_batch(original_count, recovery_count, shard_bytes, nstripes, d
     _check(lib().rs16_encode_device_batch(eng.h, original_count, recovery_count, shard_bytes, nstripes,
                                           Engine._ptr(d_original), original_stride, Engine._ptr(d_recovery),
                                           recovery_stride, stream, C.byref(err)), err)
+
+
+def decode_device_batch(original_count, recovery_count, shard_bytes, nstripes, d_original, original_stride,
+                        d_original_received, d_recovery, recovery_stride, d_recovery_received,
+                        original_received_count, recovery_received_count, stream=None,
+                        engine: Optional[Engine] = None):
+    """rs16_decode_device_batch: nstripes stripes with one shared erasure pattern."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_decode_device_batch(eng.h, original_count, recovery_count, shard_bytes, nstripes,
+                                          Engine._ptr(d_original), original_stride, Engine._ptr(d_original_received),
+                                          Engine._ptr(d_recovery), recovery_stride, Engine._ptr(d_recovery_received),
+                                          original_received_count, recovery_received_count, stream, C.byref(err)), err)
 
 
 def decode_device(original_count, recovery_count, shard_bytes, d_original, d_original_received, d_recovery,

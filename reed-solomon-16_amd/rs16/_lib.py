@@ -80,6 +80,7 @@ SIGNATURES = {
     "rs16_decoder_is_high_rate": (_i, [_p]),
     "rs16_encode_device": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _e]),
     "rs16_encode_device_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _sz, _p, _e]),
+    "rs16_decode_device_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _p, _sz, _p, _sz, _sz, _p, _e]),
     "rs16_decode_device": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _p, _sz, _sz, _p, _e]),
     "rs16_decode_check": (_i, [_p, _p, _e]),
     "rs16_device_alloc": (_p, [_p, _sz, _e]),

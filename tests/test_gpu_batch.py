@@ -47,3 +47,48 @@ def test_batch_errors_and_empty():
     with pytest.raises(rs16.Error) as e:
         rs16.encode_device_batch(2, 2, 100, 2, d.ptr, 256, d.ptr, 256, engine=eng)
     assert e.value.kind == "InvalidShardSize"
+
+
+@pytest.mark.parametrize("k,m,sb,n,pattern", [
+    (1000, 1000, 1024, 6, "all"), (1000, 1000, 1024, 5, "tail"), (100, 100, 1024, 9, "all"),
+    (100, 300, 192, 4, "scatter"), (4096, 4096, 128, 3, "tail"), (4096, 4096, 128, 3, "all"),
+    (2000, 3000, 64, 4, "scatter"), (3, 5, 64, 7, "all"), (3000, 1000, 64, 3, "scatter"),
+    (300, 3000, 64, 3, "all"),
+])
+def test_decode_batch_shared_pattern(k, m, sb, n, pattern):
+    # every stripe lost the same originals (a failed device); the restored
+    # originals of every stripe must be the originals, and the recovery rows
+    # and the received originals must stay untouched
+    eng = rs16.default_engine()
+    pad = 64
+    so, sr = k * sb + pad, m * sb + pad
+    stripes = [generate_original(k, sb, 17 * i + k) for i in range(n)]
+    recs = [O.encode(k, m, o) for o in stripes]
+    lost = min(k, m)
+    om = np.ones(k, bool)
+    if pattern == "all":
+        om[:lost] = False
+    elif pattern == "tail":
+        om[k - max(1, lost // 100):] = False
+    else:
+        om[np.random.default_rng(k + m).choice(k, lost // 2 + 1, replace=False)] = False
+    nlost = int((~om).sum())
+    rm = np.zeros(m, bool)
+    rm[np.random.default_rng(m).choice(m, nlost, replace=False)] = True
+    host_o = np.full(n * so, 0x3C, np.uint8)
+    host_r = np.full(n * sr, 0x3C, np.uint8)
+    for i in range(n):
+        held = stripes[i].copy()
+        held[~om] = 0xA5  # garbage in the lost slots
+        host_o[i * so:i * so + k * sb] = held.reshape(-1)
+        host_r[i * sr:i * sr + m * sb] = recs[i].reshape(-1)
+    d_o, d_r = DeviceArray.from_numpy(eng, host_o), DeviceArray.from_numpy(eng, host_r)
+    d_of = DeviceArray.from_numpy(eng, om.astype(np.uint8))
+    d_rf = DeviceArray.from_numpy(eng, rm.astype(np.uint8))
+    rs16.decode_device_batch(k, m, sb, n, d_o.ptr, so, d_of.ptr, d_r.ptr, sr, d_rf.ptr, int(om.sum()), nlost,
+                             engine=eng)
+    got = d_o.download(shape=(n * so,))
+    for i in range(n):
+        assert np.array_equal(got[i * so:i * so + k * sb].reshape(k, sb), stripes[i]), i
+        assert (got[i * so + k * sb:(i + 1) * so] == 0x3C).all(), i
+    assert np.array_equal(d_r.download(shape=(n * sr,)), host_r)
