@@ -216,7 +216,8 @@ int rs16_encode_device(rs16_engine* eng, size_t original_count, size_t recovery_
  * one call (many objects, each its own codeword set; SURVEY.md 8(f)3
  * "batched independent codewords"): stripe i's original_count shards at
  * d_original + i * original_stride bytes, its recovery_count shards written
- * at d_recovery + i * recovery_stride (strides >= count * shard_bytes).
+ * at d_recovery + i * recovery_stride (strides >= count * shard_bytes and
+ * multiples of 64, else RS16_INVALID_ARGUMENT).
  * Every stripe's result equals rs16_encode_device on it alone.  High-rate
  * stripes with original_count <= next_pow2(recovery_count) -- every stripe
  * with original_count <= recovery_count -- run batched, each pass launch
@@ -246,7 +247,8 @@ int rs16_decode_device(rs16_engine* eng, size_t original_count, size_t recovery_
  * shards -- the case of a failed device, which holds the same shard index of
  * every stripe: the received flags and counts are shared, stripe i's
  * original slots at d_original + i * original_stride bytes (lost ones
- * restored in place), its recovery at d_recovery + i * recovery_stride.
+ * restored in place), its recovery at d_recovery + i * recovery_stride
+ * (strides as for rs16_encode_device_batch).
  * One eval_poly for all, every pass launch covering all stripes.  Every
  * stripe's result equals rs16_decode_device on it alone. */
 int rs16_decode_device_batch(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,

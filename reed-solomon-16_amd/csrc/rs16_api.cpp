@@ -898,7 +898,9 @@ extern "C" int rs16_encode_device_batch(rs16_engine* e, size_t k, size_t m, size
     bool high;
     if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
     if (nstripes == 0) return set_error(err, RS16_OK);
-    if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S)
+    // (strides in whole 64-byte blocks, as shard sizes: every row stays aligned)
+    if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S || original_stride % 64 ||
+        recovery_stride % 64)
         return set_error(err, RS16_INVALID_ARGUMENT);
     const size_t chunk = next_pow2(m);
     // one launch holds < 2^32 tiles; stay far below
@@ -1201,8 +1203,8 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
     if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
     if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
     if (nstripes == 0 || orig_recv == k) return set_error(err, RS16_OK);
-    if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S ||
-        nstripes > ((size_t)1 << 20))
+    if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S || original_stride % 64 ||
+        recovery_stride % 64 || nstripes > ((size_t)1 << 20))
         return set_error(err, RS16_INVALID_ARGUMENT);
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);

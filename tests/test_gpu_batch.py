@@ -45,8 +45,18 @@ def test_batch_errors_and_empty():
         rs16.encode_device_batch(2, 2, 64, 2, d.ptr, 64, d.ptr, 128, engine=eng)  # stride < k * S
     assert e.value.kind == "InvalidArgument"
     with pytest.raises(rs16.Error) as e:
+        rs16.encode_device_batch(2, 2, 64, 2, d.ptr, 160, d.ptr, 128, engine=eng)  # stride not in 64 B blocks
+    assert e.value.kind == "InvalidArgument"
+    with pytest.raises(rs16.Error) as e:
         rs16.encode_device_batch(2, 2, 100, 2, d.ptr, 256, d.ptr, 256, engine=eng)
     assert e.value.kind == "InvalidShardSize"
+    f = DeviceArray(eng, 64)
+    with pytest.raises(rs16.Error) as e:  # (decode: the reference's NotEnoughShards first)
+        rs16.decode_device_batch(2, 2, 64, 2, d.ptr, 128, f.ptr, d.ptr, 128, f.ptr, 0, 1, engine=eng)
+    assert e.value.kind == "NotEnoughShards"
+    with pytest.raises(rs16.Error) as e:
+        rs16.decode_device_batch(2, 2, 64, 2, d.ptr, 96, f.ptr, d.ptr, 128, f.ptr, 0, 2, engine=eng)
+    assert e.value.kind == "InvalidArgument"
 
 
 @pytest.mark.parametrize("k,m,sb,n,pattern", [
