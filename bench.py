@@ -600,6 +600,34 @@ def main():
                 "lost_originals": lost3}
         extra["rate_paths"] = rp
 
+    if not args.no_extra and world > 1 and S % (64 * world) == 0:
+        # Strong scaling of ONE stripe (the 1 KiB configs over N
+        # GPUs as S / N byte-column slices): every rank encodes and decodes its
+        # column slice of the same 32768:32768 x 1 KiB stripe (here: slice r
+        # of this rank's originals; every slice is its own codeword set); the
+        # whole stripe is done when the slowest rank is.
+        off_s, w_s = rs16.column_slice(S, world, rank)
+        sl = np.ascontiguousarray(original[:, off_s:off_s + w_s])
+        d_so, d_sr, d_sx = DeviceArray.from_numpy(eng, sl), DeviceArray(eng, m * w_s), DeviceArray(eng, k * w_s)
+        fo_s = DeviceArray.from_numpy(eng, of)
+        fr_s = DeviceArray.from_numpy(eng, rf)
+
+        def slice_step():
+            rs16.encode_device(k, m, w_s, d_so.ptr, d_sr.ptr, engine=eng)
+            rs16.decode_device(k, m, w_s, d_sx.ptr, fo_s.ptr, d_sr.ptr, fr_s.ptr, k - loss, loss, engine=eng)
+
+        slice_step()
+        if loss == k:
+            assert np.array_equal(d_sx.download(shape=(k, w_s)), sl), "column-slice decode did not restore"
+        for _ in range(args.warmup):
+            slice_step()
+        ts = timed(slice_step, args.steps)
+        extra["one_stripe_column_slices"] = {
+            "workload": f"one {k}:{m} x {S} B stripe, {w_s} B column slice per rank, encode + "
+                        f"{'100%' if loss == k else 'partial'}-loss decode (strong scaling)",
+            "gib_s": step_bytes * args.steps / ts / GIB, "ms_per_step": ts / args.steps * 1e3,
+            "slice_bytes": w_s}
+
     if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
         extra["configs4_rccl"] = configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, args.steps)
 
