@@ -4,10 +4,15 @@
 // rounds of: (optionally) store 32 KiB per workgroup, wave stores done,
 // workgroup barrier, thread 0 adds 1 to a device counter with an agent-scope
 // release, spins (bounded) on an agent-scope acquire load until the counter
-// reaches the round's target, workgroup barrier.  Reported: us per round,
+// reaches the round's target, workgroup barrier.  RELAXED_POLL (default):
+// relaxed polling loads and one acquire fence after the wait; 0: every
+// polling load an acquire (a cache invalidate per poll).  Reported: us per round,
 // against K rounds of the same work without the wait.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#ifndef RELAXED_POLL
+#define RELAXED_POLL 1  // poll with relaxed loads, one acquire fence after the wait
+#endif
 
 template <bool WAIT, bool STORE>
 __global__ void __launch_bounds__(256) sync_k(unsigned* cnt, uint4* buf, int rounds, unsigned nwg) {
@@ -26,9 +31,12 @@ __global__ void __launch_bounds__(256) sync_k(unsigned* cnt, uint4* buf, int rou
                 __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned target = (unsigned)(r + 1) * nwg;
                 for (unsigned i = 0; i < (1u << 22); i++) {
-                    if (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+                    if (__hip_atomic_load(cnt, RELAXED_POLL ? __ATOMIC_RELAXED : __ATOMIC_ACQUIRE,
+                                          __HIP_MEMORY_SCOPE_AGENT) >= target)
+                        break;
                     __builtin_amdgcn_s_sleep(1);
                 }
+                if (RELAXED_POLL) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             }
             __syncthreads();
         }
