@@ -47,6 +47,14 @@
 //   DEC_MID to read those rows as zero and to skip the IFFT groups whose rows
 //   all are, and DEC_LAST that its z term is zero (y = u + L(z) = u).  At
 //   100 % original loss this is the whole original half of the decode work.
+//
+//   Zero twiddles: the sentinel sits exactly at skew indices 2^i - 1, i.e. at
+//   the first group of each layout-B layer of the two-direction passes; those
+//   groups run the XOR half of the butterfly only (wave-uniform test).
+//
+//   Batched stripes (PassArgs::stripe_tiles): one launch covers independent
+//   stripes of one geometry; a workgroup's tile index splits into (stripe,
+//   tile within the stripe) and the stripe displaces its array pointers.
 #include "rs16_internal.hpp"
 
 namespace rs16 {
