@@ -102,3 +102,26 @@ def test_decode_batch_shared_pattern(k, m, sb, n, pattern):
         assert np.array_equal(got[i * so:i * so + k * sb].reshape(k, sb), stripes[i]), i
         assert (got[i * so + k * sb:(i + 1) * so] == 0x3C).all(), i
     assert np.array_equal(d_r.download(shape=(n * sr,)), host_r)
+
+
+@pytest.mark.parametrize("k,m,n", [(2, 3, 2048), (4, 4, 1000), (16, 16, 777)])
+def test_batch_many_small_stripes(k, m, n):
+    # thousands of tiny stripes in one call (large grids, stripe counts that
+    # are not multiples of 8): encode, then decode with every original lost
+    eng = rs16.default_engine()
+    sb = 64
+    rng = np.random.default_rng(n)
+    orig = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    d_o = DeviceArray.from_numpy(eng, orig.reshape(-1))
+    d_r = DeviceArray(eng, n * m * sb)
+    rs16.encode_device_batch(k, m, sb, n, d_o.ptr, k * sb, d_r.ptr, m * sb, engine=eng)
+    rec = d_r.download(shape=(n, m, sb))
+    for i in (0, 1, n // 2, n - 1):
+        assert np.array_equal(rec[i], O.encode(k, m, orig[i])), i
+    d_x = DeviceArray.from_numpy(eng, np.zeros(n * k * sb, np.uint8))
+    fo = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+    rm = np.zeros(m, np.uint8)
+    rm[:k] = 1
+    fr = DeviceArray.from_numpy(eng, rm)
+    rs16.decode_device_batch(k, m, sb, n, d_x.ptr, k * sb, fo.ptr, d_r.ptr, m * sb, fr.ptr, 0, k, engine=eng)
+    assert np.array_equal(d_x.download(shape=(n, k, sb)), orig)
