@@ -134,7 +134,7 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
 }
 extern "C" int rs16_set_diagnostics(int flags) {
     const int old = g_diag;
-    g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL);
+    g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN);
     return old;
 }
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
@@ -142,7 +142,7 @@ extern "C" const char* rs16_prog_name(int prog) {
     static const char* names[] = {"GEN_FFT",   "GEN_IFFT",   "ENC_FIRST",     "ENC_MID",
                                   "ENC_LAST",  "ENC_SINGLE", "DEC_FIRST",     "DEC_MID",
                                   "DEC_LAST",  "DEC_SINGLE", "DEC_HALF_LAST", "DEC_HALF_SINGLE",
-                                  "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY"};
+                                  "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY", "COL_ENC", "COL_DEC"};
     static_assert(sizeof names / sizeof names[0] == NUM_PROF, "profiling names");
     return (prog >= 0 && prog < NUM_PROF) ? names[prog] : "?";
 }

@@ -215,6 +215,35 @@ int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStr
     return prof_end(prof, s, ev, err);
 }
 
+bool rs16_engine::col_ok(int L, size_t S, size_t nstripes) const {
+    return col_rows_ok((uint32_t)L) && (S / 8) * nstripes <= col_max_quads && !(g_diag & DIAG_NO_COLUMN);
+}
+
+ColArgs rs16_engine::col_args() const {
+    ColArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.skew_tab = d_skew_tab;
+    a.mul_tab = d_mul_tab;
+    a.zero = d_zero_sink;
+    a.elog = (const uint32_t*)ws_elog.p;
+    a.nstripes = 1;
+    return a;
+}
+
+int rs16_engine::col(const ColArgs& a, int L, bool dec, hipStream_t s, rs16_error* err) {
+    hipEvent_t ev;
+    const int prof = dec ? PROF_COL_DEC : PROF_COL_ENC;
+    if (int rc = prof_begin(s, &ev, err)) return rc;
+    if (stamp_buf && stamp_prof == prof) {
+        ColArgs b = a;
+        b.stamps = (uint64_t*)stamp_buf;
+        RS16_HIP(launch_col(b, (uint32_t)L, dec, s));
+    } else {
+        RS16_HIP(launch_col(a, (uint32_t)L, dec, s));
+    }
+    return prof_end(prof, s, ev, err);
+}
+
 // Engine::fft over 2^L rows: L <= 8 in one pass; otherwise the high
 // (L - L/2) row bits as a strided pass, then the low L/2 bits contiguous.
 int rs16_engine::fft(uint8_t* data, size_t S, size_t pos, size_t size, size_t skew_delta, hipStream_t s,
@@ -286,6 +315,22 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
         a.S_out = S_user;
         RS16_PASS(ENC_SINGLE, L, a, batch(1, 0, bs_rec, bs_orig), s);
         return RS16_OK;
+    }
+    if (col_ok(L, S, nst)) {
+        // 512 / 1024-row chunks: the whole encode in one launch (rs16_col.hip)
+        ColArgs c = col_args();
+        c.in = d_orig;
+        c.out = d_rec;
+        c.S_in = c.S_out = S_user;
+        c.qrow = (uint32_t)(S / 8);
+        c.nstripes = ns;
+        c.bs_in = bs_orig;
+        c.bs_out = bs_rec;
+        c.in_rows = (uint32_t)k;
+        c.out_rows = (uint32_t)m;
+        c.skew_ifft = (uint32_t)chunk;
+        c.skew_fft = 0;
+        return col(c, L, false, s, err);
     }
     // odd L: the extra row bit goes to the strided two-direction pass (an
     // 8 / 7 / 8 split measured 2-3 us slower per encode)
@@ -363,6 +408,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // (one kernel less) -- except the one-pass half-transform decode, whose
     // gather and reveal rows lie in different blocks.
     const bool small = g.high && g.n <= 2048 && !(g_diag & DIAG_EVAL_FULL);
+    // (the column codec's half decodes of 2^9 / 2^10 rows finish it too)
     elog_fused = !(half_decode(g) && ilog2(g.n) - 1 <= 8);
     if (small) {
         // erasures are zero from row n on: only n/256 live blocks (rs16_misc.hip)
@@ -439,6 +485,24 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
             a.ework = nullptr;  // (decode_eval did the whole eval_poly)
             RS16_PASS(DEC_HALF_SINGLE, Lh, a, batch(1, 0, 0, 0), s);
             return RS16_OK;
+        }
+        if (col_ok(Lh, S, ns)) {
+            // 512 / 1024-row halves: the whole decode in one launch (rs16_col.hip)
+            ColArgs c = col_args();
+            c.in = g.high ? seg_a : seg_b;
+            c.flags = g.high ? flags_a : flags_b;
+            c.in_rows = g.high ? g.a_count : g.b_count;
+            c.out = rest;
+            c.S_in = c.S_out = S_user;
+            c.qrow = (uint32_t)(S / 8);
+            c.nstripes = ns;
+            c.bs_in = g.high ? bs_a : bs_b;
+            c.bs_out = bs_rest;
+            c.out_rows = orig;
+            c.base_in = c.skew_ifft = src;
+            c.base_out = c.skew_fft = dst;
+            c.elog = (const uint32_t*)ws_work32.p;  // (eval_poly without its last H_lo: elog_fused)
+            return col(c, Lh, true, s, err);
         }
         const int lo = Lh / 2, hi = Lh - lo;
         a.lo = 0;
@@ -579,6 +643,19 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
         RS16_HIP(launch_copy_chunks(Z, S, nch, s));
         if (d_rec != Z) RS16_HIP(hipMemcpy2DAsync(d_rec, S_user, Z, S, S, m, hipMemcpyDeviceToDevice, s));
         return RS16_OK;
+    }
+    if (nch == 1 && col_ok(L, S, 1)) {
+        // one recovery chunk of 512 / 1024 rows: one launch (rs16_col.hip)
+        ColArgs c = col_args();
+        c.in = d_orig;
+        c.out = d_rec;
+        c.S_in = c.S_out = S_user;
+        c.qrow = (uint32_t)(S / 8);
+        c.in_rows = (uint32_t)k;
+        c.out_rows = (uint32_t)m;
+        c.skew_ifft = 0;
+        c.skew_fft = (uint32_t)chunk;
+        return col(c, L, false, s, err);
     }
     RS16_HIP(ws_u.reserve(chunk * S));
     uint8_t* U = (uint8_t*)ws_u.p;

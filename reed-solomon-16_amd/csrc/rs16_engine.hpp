@@ -189,6 +189,14 @@ struct rs16_engine {
     // The half-transform decode applies (every original lost, originals
     // segment = one half of the work rows).
     static bool half_decode(const rs16::DecodeGeom& g);
+    // One-launch codec (rs16_col.hip) for transforms of 2^9 / 2^10 rows:
+    // used when the launch has at most col_max_quads quad columns (x
+    // stripes); wider launches take the pass codec, whose tiles share each
+    // twiddle table over 32 quad columns.
+    uint32_t col_max_quads = 1u << 30;
+    bool col_ok(int L, size_t S, size_t nstripes) const;
+    int col(const rs16::ColArgs& a, int L, bool dec, hipStream_t s, rs16_error* err);
+    rs16::ColArgs col_args() const;
     // Multi-chunk encoders (high rate with k > chunk, low rate): every chunk's
     // transform in one batched set of launches.  d_orig rows have pitch
     // S_user, Z is the work space (work_count x S; may be d_orig), the

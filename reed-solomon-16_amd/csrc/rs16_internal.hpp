@@ -47,7 +47,14 @@ enum Prog : int {
 // Profiling ids (rs16_engine_set_profiling): the programs, then the passes
 // of the half-transform decode that reuse DEC_FIRST / ENC_MID kernels, then
 // the eval_poly kernels of a decode.
-enum ProfId : int { PROF_DEC_HALF_FIRST = NUM_PROGS, PROF_DEC_HALF_MID, PROF_EVAL_POLY, NUM_PROF };
+enum ProfId : int {
+    PROF_DEC_HALF_FIRST = NUM_PROGS,
+    PROF_DEC_HALF_MID,
+    PROF_EVAL_POLY,
+    PROF_COL_ENC,  // one-launch codec (rs16_col.hip): encode
+    PROF_COL_DEC,  // one-launch codec: half-transform decode
+    NUM_PROF
+};
 
 struct PassArgs {
     uint8_t* out;              // plain store base (row 0 of the transform)
@@ -133,6 +140,35 @@ struct PassArgs {
     uint32_t in_rows_mask;
 };
 
+// One-launch codec for 2^9 / 2^10-row transforms (rs16_col.hip): one
+// workgroup per quad column (x stripe) runs the whole encode or
+// half-transform decode with the column resident in registers / LDS.
+//   ENC: out[0, out_rows) = FFT_skew_fft(IFFT_skew_ifft(rows [0, in_rows) of in, zero above))
+//   DEC: x[r] = received(r) ? in[r] * e[base_in + r] : 0 (received: r < in_rows
+//        and flags[r], flags nullptr = all), out[r] = FFT(IFFT(x))[r] *
+//        (65535 - e[base_out + r]) for r < out_rows; e = the erasure logs of
+//        the 2^(L+1) work rows, whose last 256-point FWHT the kernel does
+//        itself: elog = eval_poly's output without it (the engine's ework)
+struct ColArgs {
+    const uint8_t* in;
+    const uint8_t* flags;
+    uint8_t* out;
+    const uint32_t* elog;
+    const uint32_t* skew_tab;
+    const uint32_t* mul_tab;
+    const uint8_t* zero;
+    uint64_t S_in, S_out;       // row strides of in / out
+    uint32_t qrow;              // quad columns per row (width / 8)
+    uint32_t nstripes;          // stripes (in / out displaced by bs_in / bs_out bytes each)
+    uint32_t in_rows, out_rows;
+    uint32_t skew_ifft, skew_fft;
+    uint32_t base_in, base_out;
+    uint64_t bs_in, bs_out;
+    uint64_t* stamps;           // RS16_STAMPS builds: phase timeline (rs16_engine_set_stamps)
+};
+int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec covers
+hipError_t launch_col(const ColArgs& a, uint32_t L, bool dec, hipStream_t s);
+
 // Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):
 // alternative code paths kept for tests and measurements, never needed for
 // correct results.  0 = the shipped behaviour.
@@ -140,6 +176,7 @@ enum DiagFlags : int {
     DIAG_FORCE_VOFF64 = 1,    // 64-bit lane offsets in every pass (PassArgs::voff32 = 0)
     DIAG_EVAL_TWO_KERNEL = 2, // eval_poly: two-kernel form even when the one-kernel form applies
     DIAG_EVAL_FULL = 4,       // eval_poly: the full 65536-point form even for n <= 2048
+    DIAG_NO_COLUMN = 8,       // 2^9 / 2^10-row transforms through the pass codec (rs16_col.hip off)
 };
 extern int g_diag;
 

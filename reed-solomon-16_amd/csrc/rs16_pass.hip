@@ -56,6 +56,7 @@
 //   stripes of one geometry; a workgroup's tile index splits into (stripe,
 //   tile within the stripe) and the stripe displaces its array pointers.
 #include "rs16_internal.hpp"
+#include "rs16_fwht.hpp"
 
 namespace rs16 {
 
@@ -451,29 +452,6 @@ template <int NT> __device__ __forceinline__ void fwht256_tile(uint32_t* s) {
     }
     __syncthreads();
 }
-// The same 256-point FWHT by one wave in registers: lane l holds
-// v[j] = x[l + 64 j]; distances 1..32 are lane pairs (shuffles), 64 and 128
-// register pairs.  Residues equal fwht256_tile's (every consumer of these
-// logs treats 65535 and 0 alike, exp[65535] == exp[0]).
-__device__ __forceinline__ void fwht256_wave(uint32_t (&v)[4]) {
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const bool hi = lane & d;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t p = (uint32_t)__shfl_xor((int)v[j], d);
-            v[j] = hi ? sub_mod(p, v[j]) : add_mod(v[j], p);
-        }
-    }
-    uint32_t a = add_mod(v[0], v[1]), b = sub_mod(v[0], v[1]);
-    uint32_t c = add_mod(v[2], v[3]), e = sub_mod(v[2], v[3]);
-    v[0] = add_mod(a, c);
-    v[2] = sub_mod(a, c);
-    v[1] = add_mod(b, e);
-    v[3] = sub_mod(b, e);
-}
-
 // Layers for k-bits [KB0, KB1) held in registers of layout LB, as a
 // compile-time sequence of twiddle groups (step s, index gi).
 // No per-group action (GroupLoop's default).

@@ -28,6 +28,8 @@ from rs16.device import DeviceArray  # noqa: E402
 from rs16.util import generate_original  # noqa: E402
 
 PH = ["start", "loads", "staged", "A-layers", "switch1", "dir1", "fd", "B-fft", "switch2", "last", "stores", "drain"]
+# the column codec (rs16_col.hip cstamp)
+PH_COL = ["start", "issued", "staged", "iblk0", "iblk2", "ifft", "fblk0", "fblk2", "fxchg3", "fft", "stores", "drain"]
 
 
 def main():
@@ -87,7 +89,8 @@ def main():
         phases = {}
         for a, b in zip(rec, rec[1:]):
             dur = (st[:, b] - st[:, a]) / ghz / 1000.0  # us
-            phases[f"{PH[a]}->{PH[b]}"] = round(float(np.median(dur)), 2)
+            ph = PH_COL if name.startswith("COL") else PH
+            phases[f"{ph[a]}->{ph[b]}"] = round(float(np.median(dur)), 2)
         out[name] = {
             "workgroups": int(len(st)),
             "clock_ghz_median": round(float(np.median(ghz)), 3),

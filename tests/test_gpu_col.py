@@ -1,0 +1,185 @@
+"""GPU parity of the one-launch column codec (rs16_col.hip): every encode whose
+transform has 512 or 1024 rows and every half-transform decode (all originals
+lost) over 512 / 1024-row halves runs as one kernel per call.  Its results
+must equal the oracle's (the NoSimd restatement, src/rate/rate_high.rs:44-83,
+src/rate/rate_low.rs:44-83) and the pass codec's (rs16.DIAG_NO_COLUMN) bit for
+bit: high and low rate, partial chunks, every shard width class, column
+slices of wider arrays, batched stripes, the in-place work buffer of the Rate
+API, and decodes with lost recovery shards and garbage in the lost slots.
+"""
+import numpy as np
+import pytest
+
+import oracle_bind as O
+import rs16
+from rs16.device import DeviceArray
+from rs16.util import generate_original
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return rs16.default_engine()
+
+
+@pytest.fixture
+def no_column():
+    old = rs16.set_diagnostics(rs16.DIAG_NO_COLUMN)
+    yield
+    rs16.set_diagnostics(old)
+
+
+def dev_encode(eng, original, m):
+    k, sb = original.shape
+    d_orig = DeviceArray.from_numpy(eng, original)
+    d_rec = DeviceArray.from_numpy(eng, np.full((m, sb), 0x5A, np.uint8))
+    rs16.encode_device(k, m, sb, d_orig.ptr, d_rec.ptr, engine=eng)
+    return d_rec.download(shape=(m, sb))
+
+
+def dev_decode(eng, original, recovery, orig_mask, rec_mask):
+    k, sb = original.shape
+    m = recovery.shape[0]
+    holes = original.copy()
+    holes[~orig_mask] = 0xA5
+    d_orig = DeviceArray.from_numpy(eng, holes)
+    d_rec = DeviceArray.from_numpy(eng, recovery)
+    d_of = DeviceArray.from_numpy(eng, orig_mask.astype(np.uint8))
+    d_rf = DeviceArray.from_numpy(eng, rec_mask.astype(np.uint8))
+    rs16.decode_device(k, m, sb, d_orig.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, int(orig_mask.sum()),
+                       int(rec_mask.sum()), engine=eng, check=True)
+    return d_orig.download(shape=(k, sb))
+
+
+# (k, m): chunk = 512 / 1024 rows on the high-rate side, and low-rate cases
+# whose one recovery chunk is 512 / 1024 rows
+CASES = [(1, 257), (100, 300), (257, 512), (512, 512), (300, 1000), (1000, 1000), (1024, 1024), (511, 513),
+         (700, 600), (1000, 520), (1024, 600), (600, 1024)]
+
+
+@pytest.mark.parametrize("k,m", CASES)
+@pytest.mark.parametrize("sb", [64, 1024])
+def test_col_encode_vs_oracle(eng, k, m, sb):
+    original = generate_original(k, sb, k + 7 * m + sb)
+    assert np.array_equal(dev_encode(eng, original, m), O.encode(k, m, original))
+
+
+@pytest.mark.parametrize("sb", [192, 4096, 65536])
+def test_col_encode_widths(eng, sb):
+    k, m = 1000, 1000
+    original = generate_original(k, sb, sb)
+    assert np.array_equal(dev_encode(eng, original, m), O.encode(k, m, original))
+
+
+@pytest.mark.parametrize("k,m", [(1000, 1000), (300, 1000), (512, 512), (1024, 600)])
+def test_col_matches_pass_codec(eng, k, m, no_column):
+    # (the fixture sets DIAG_NO_COLUMN for the reference run; the column run
+    # switches it off around its own call)
+    sb = 256
+    original = generate_original(k, sb, 3 * k + m)
+    want = dev_encode(eng, original, m)
+    old = rs16.set_diagnostics(0)
+    try:
+        got = dev_encode(eng, original, m)
+    finally:
+        rs16.set_diagnostics(old)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("k,m", [(1000, 1000), (512, 512), (257, 300), (100, 1000), (1024, 1024), (600, 1024),
+                                 (1000, 520)])
+@pytest.mark.parametrize("lost_rec", [0, 5])
+def test_col_half_decode(eng, k, m, lost_rec):
+    """Every original lost, recovery shards given (some of them lost too):
+    the half-transform decode; restored bit for bit."""
+    if m - lost_rec < k:
+        pytest.skip("not enough recovery shards")
+    sb = 128
+    original = generate_original(k, sb, k + m)
+    recovery = O.encode(k, m, original)
+    om = np.zeros(k, bool)
+    rm = np.ones(m, bool)
+    rng = np.random.default_rng(k * m)
+    if lost_rec:
+        rm[rng.choice(m, lost_rec, replace=False)] = False
+    assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+
+
+@pytest.mark.parametrize("rate", ["high", "low"])
+@pytest.mark.parametrize("k,m", [(1000, 1000), (512, 300), (300, 512)])
+def test_col_rate_api_in_place(eng, rate, k, m):
+    """The Rate API's work buffer: originals, recovery and restored rows
+    share one array (in == out for the column encode)."""
+    sb = 64
+    if not rs16.supports(k, m, rate):
+        pytest.skip("unsupported")
+    original = generate_original(k, sb, k ^ m)
+    enc = rs16.RateEncoder(k, m, sb, rate, engine=eng)
+    for o in original:
+        enc.add_original_shard(o)
+    with enc.encode() as res:
+        rec = np.stack([np.frombuffer(r, np.uint8) for r in res.recovery_iter()])
+    assert np.array_equal(rec, O.encode(k, m, original, rate=rate))
+    # lose the first min(k, m) originals (all of them when k <= m: the half decode)
+    lost = min(k, m)
+    dec = rs16.RateDecoder(k, m, sb, rate, engine=eng)
+    for i in range(lost, k):
+        dec.add_original_shard(i, original[i])
+    for i in range(lost):
+        dec.add_recovery_shard(i, rec[i])
+    with dec.decode() as res:
+        got = dict(res.restored_original_iter())
+    assert sorted(got) == list(range(lost))
+    assert all(np.array_equal(np.frombuffer(got[i], np.uint8), original[i]) for i in range(lost))
+
+
+@pytest.mark.parametrize("k,m,n", [(1000, 1000, 5), (512, 512, 3), (300, 1000, 4)])
+def test_col_batched_stripes(eng, k, m, n):
+    sb, pad = 128, 64
+    so, sr = k * sb + pad, m * sb + pad
+    stripes = [generate_original(k, sb, 11 * i + k) for i in range(n)]
+    host_o = np.full(n * so, 0xEE, np.uint8)
+    for i, o in enumerate(stripes):
+        host_o[i * so:i * so + k * sb] = o.reshape(-1)
+    d_o = DeviceArray.from_numpy(eng, host_o)
+    d_r = DeviceArray.from_numpy(eng, np.full(n * sr, 0x77, np.uint8))
+    rs16.encode_device_batch(k, m, sb, n, d_o.ptr, so, d_r.ptr, sr, engine=eng)
+    got = d_r.download(shape=(n * sr,))
+    recs = []
+    for i, o in enumerate(stripes):
+        want = O.encode(k, m, o)
+        recs.append(want)
+        assert np.array_equal(got[i * sr:i * sr + m * sb].reshape(m, sb), want), i
+        assert (got[i * sr + m * sb:(i + 1) * sr] == 0x77).all(), i
+    # batched half decode: every original of every stripe lost
+    d_o2 = DeviceArray.from_numpy(eng, np.full(n * so, 0xA5, np.uint8))
+    d_of = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+    d_rf = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+    rs16.decode_device_batch(k, m, sb, n, d_o2.ptr, so, d_of.ptr, d_r.ptr, sr, d_rf.ptr, 0, m, engine=eng)
+    back = d_o2.download(shape=(n * so,))
+    for i, o in enumerate(stripes):
+        assert np.array_equal(back[i * so:i * so + k * sb].reshape(k, sb), o), i
+        assert (back[i * so + k * sb:(i + 1) * so] == 0xA5).all(), i
+
+
+@pytest.mark.parametrize("slices", [2, 3])
+def test_col_column_slices(slices):
+    """Column slices of wider arrays (row stride > slice width; rs16_engine_set_slices):
+    every slice is its own column launch, encode and half decode."""
+    eng = rs16.Engine(0)
+    eng.set_slices(slices)
+    k, m, sb = 1000, 1000, 1024 + 64 * slices
+    original = generate_original(k, sb, 99 + slices)
+    recovery = dev_encode(eng, original, m)
+    assert np.array_equal(recovery, O.encode(k, m, original))
+    om, rm = np.zeros(k, bool), np.ones(m, bool)
+    assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+
+
+def test_col_host_multi(eng):
+    k, m, sb = 1000, 1000, 1024
+    original = generate_original(k, sb, 98)
+    rec = np.zeros((m, sb), np.uint8)
+    rs16.encode_host_multi(k, m, sb, original, rec, [eng, rs16.Engine(0)])
+    assert np.array_equal(rec, O.encode(k, m, original))
