@@ -377,8 +377,9 @@ enum {
     RS16_DIAG_FORCE_VOFF64 = 1,    /* 64-bit per-lane HBM offsets in every pass */
     RS16_DIAG_EVAL_TWO_KERNEL = 2, /* eval_poly: the two-kernel form everywhere */
     RS16_DIAG_EVAL_FULL = 4,       /* eval_poly: the full 65536-point form for n <= 2048 */
-    RS16_DIAG_NO_COLUMN = 8        /* 512 / 1024-row transforms through the pass codec instead of
+    RS16_DIAG_NO_COLUMN = 8,       /* 512 / 1024-row transforms through the pass codec instead of
                                       the one-launch column codec */
+    RS16_DIAG_FORCE_COLUMN = 16    /* ... through the column codec at any shard width / stripe count */
 };
 int rs16_set_diagnostics(int flags);
 

@@ -134,7 +134,7 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
 }
 extern "C" int rs16_set_diagnostics(int flags) {
     const int old = g_diag;
-    g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN);
+    g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN);
     return old;
 }
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
@@ -231,11 +231,15 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
     if ((he = hipMalloc(&e->d_skew_tab, (size_t)GF_ORDER * TAB_DWORDS * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_mul_tab, t.mul_tab.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_log_walsh, GF_ORDER * 2)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_col_img, COL_IMG_DWORDS * 4)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_col_v, t.col_v.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_zero_sink, RS16_ZERO_BYTES + RS16_SINK_BYTES)) != hipSuccess) return fail(he);
     if ((he = hipMemset(e->d_zero_sink, 0, RS16_ZERO_BYTES)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_skew_tab, t.skew_tab.data(), t.skew_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_mul_tab, t.mul_tab.data(), t.mul_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_log_walsh, t.log_walsh.data(), GF_ORDER * 2, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
+    if ((he = hipMemcpy(e->d_col_img, t.col_img.data(), COL_IMG_DWORDS * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
+    if ((he = hipMemcpy(e->d_col_v, t.col_v.data(), t.col_v.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     set_error(err, RS16_OK);
     return e;
 }
@@ -278,6 +282,8 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     if (e->sl_fork) (void)hipEventDestroy(e->sl_fork);
     if (e->d_skew_tab) (void)hipFree(e->d_skew_tab);
     if (e->d_mul_tab) (void)hipFree(e->d_mul_tab);
+    if (e->d_col_img) (void)hipFree(e->d_col_img);
+    if (e->d_col_v) (void)hipFree(e->d_col_v);
     if (e->d_log_walsh) (void)hipFree(e->d_log_walsh);
     if (e->d_zero_sink) (void)hipFree(e->d_zero_sink);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1009,7 +1015,7 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
     RS16_HIP(hipMemcpyAsync(d_rf, recovery_received, m, hipMemcpyHostToDevice, e->stream));
     const uint8_t* fa = high ? d_rf : d_of;
     const uint8_t* fb = high ? d_of : d_rf;
-    if (int rc = e->decode_eval(g, fa, fb, e->stream, err)) return rc;
+    if (int rc = e->decode_eval(g, fa, fb, e->stream, err, W)) return rc;
     if (int rc = e->host_slots(err)) return rc;
     for (size_t off = 0, j = 0; off < S; off += W, j++) {
         const size_t w = std::min(W, S - off);
@@ -1121,7 +1127,7 @@ extern "C" int rs16_decode_host_multi(rs16_engine* const* engines, int n, size_t
         RS16_HIP(hipMemcpyAsync(d_rf, recovery_received, m, hipMemcpyHostToDevice, e->stream));
         const uint8_t* fa = high ? d_rf : d_of;
         const uint8_t* fb = high ? d_of : d_rf;
-        if (int rc = e->decode_eval(g, fa, fb, e->stream, err)) return rc;
+        if (int rc = e->decode_eval(g, fa, fb, e->stream, err, w)) return rc;
         if (rec_recv)
             RS16_HIP(hipMemcpy2DAsync(sl.rec.p, w, (const uint8_t*)h_recovery + off, S, w, m, hipMemcpyHostToDevice,
                                       e->stream));
@@ -1164,8 +1170,9 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
     const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
     // erasure logs once, then the passes per column slice on the slice streams
-    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err)) return rc;
+    // (one slice: the column codec may compute them itself, decode_eval)
     const int n = e->slice_count(S);
+    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, n == 1 ? S : 0)) return rc;
     if (n == 1) {
         if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
                                       (uint8_t*)e->ws_u.p, s, err))
@@ -1221,7 +1228,7 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
     const size_t bs_a = high ? recovery_stride : original_stride, bs_b = high ? original_stride : recovery_stride;
     const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
     const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
-    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err)) return rc;
+    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, S, nstripes)) return rc;
     if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
                                   (uint8_t*)e->ws_u.p, s, err, nstripes, bs_a, bs_b, original_stride))
         return rc;

@@ -25,14 +25,17 @@
 //   * 2^L / 4 threads (4 waves at L = 10, one per SIMD), 4 rows per thread.
 //     Layers go in radix-4 blocks over two row bits (b0, b1): the thread's
 //     4 rows are its index with b0 / b1 inserted, so both layers of a block
-//     are in registers; between blocks the rows move through an 8 KiB LDS
-//     image (one barrier per block: every thread writes back exactly the
-//     rows it read).  The image is XOR-swizzled (row bits 5, 6 into bits
-//     0-4) so that every block's b64 accesses are bank-conflict free.
-//   * The 2 (2^L - 1) twiddle tables of the codec (80-byte v_perm tables,
-//     rs16_gf.hpp) are staged once into LDS: both directions except the FFT's
-//     last layer (2^(L-1) tables), which is written over the IFFT's first
-//     layer once that block is done -- 128 KiB at L = 10.
+//     are in registers.  Between blocks the row bits of registers and lanes
+//     trade places inside the wave -- DPP lane swaps for lane bits 0-3,
+//     v_permlane16/32_swap for bits 4-5, no LDS and no barrier -- except
+//     around the block whose row bits are the wave index (two exchanges
+//     through an 8 KiB LDS image, XOR-swizzled so that the b64 accesses are
+//     bank-conflict free).
+//   * All 2 (2^L - 1) twiddle tables of the codec (80-byte v_perm tables,
+//     rs16_gf.hpp; 160 KiB at L = 10) are staged into LDS by LDS-DMA loads
+//     (global_load_lds_dwordx4) from contiguous images the engine builds at
+//     creation (HostTables::col_img): no VGPRs, no address arithmetic.  The
+//     FFT's last layer streams in while the IFFT runs.
 //   * The IFFT's last block and the FFT's first share their row bits: no
 //     exchange between the two directions.
 //   * Rows are loaded straight into the first block's layout and stored from
@@ -51,8 +54,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // LDS index of row r in the image (uint2 units): bits 5 and 6 are XORed
 // into bits 0-4 so that the 32 lanes of a b64 access hit 32 distinct bank
-// pairs for every block's row pattern (block bits (0,1): lane bits -> row
-// bits 2-6; (2,3): 0,1,4,5,6; (4,5): 0-3,6; (6,7), (8,9): 0-4).
+// pairs for both LDS exchanges' row patterns.
 __device__ __forceinline__ uint32_t swz(uint32_t r) {
     return r ^ (((r >> 5) & 1u) * 5u) ^ (((r >> 6) & 1u) * 26u);
 }
@@ -66,27 +68,24 @@ template <int B0, int B1> __device__ __forceinline__ uint32_t brow(uint32_t t, i
     return lo | (mid << (B0 + 1)) | (hi << (B1 + 1)) | ((uint32_t)(m & 1) << B0) | ((uint32_t)(m >> 1) << B1);
 }
 
-// LDS layout (bytes): [image 2^L x 8][A: (2^L - 1) x 80][B: (2^(L-1) - 1) x 80]
-// A holds the IFFT's tables in tile-group order (layer kb at 2^L - 2^(L-kb),
-// group j = row >> (kb + 1)), later the FFT's layer-0 tables in [0, 2^(L-1));
-// B holds the FFT's layers 1.. (tile group t at t - 2^(L-1)).
+// LDS layout (bytes), 2 (2^L - 1) x 80 = 160 KiB at L = 10:
+//   A [0, (N-1) 80)            the IFFT's tables in tile-group order (layer kb
+//                              at group N - 2^(L-kb), group j = row >> (kb+1))
+//   B [A end, + (N/2-1) 80)    the FFT's tables of groups >= N/2 (layers >= 1)
+//   C [B end, + N/2 80)        the FFT's layer-0 tables
+// The row image of the LDS exchanges (N x 8 bytes) lies over the IFFT's
+// layer-0 tables (dead after the first block); the decoder's erasure logs
+// (2N x 4 bytes) over C, before C's tables are loaded.
 template <int L> struct ColSmem {
     static constexpr int N = 1 << L;
-    static constexpr int IMG = N * 8;
-    static constexpr int A = IMG;
+    static constexpr int A = 0;
     static constexpr int B = A + (N - 1) * 80;
-    static constexpr int TABS_END = B + (N / 2 - 1) * 80;
-    // decoder: the erasure logs of the 2^(L+1) work rows (eval_poly's last H_lo, done here)
-    static constexpr int ELOG = TABS_END;
-    static constexpr int bytes(bool dec) { return TABS_END + (dec ? 2 * N * 4 : 0); }
+    static constexpr int C = B + (N / 2 - 1) * 80;
+    static constexpr int BYTES = C + (N / 2) * 80;
+    static constexpr int IMG = A;
+    static constexpr int ELOG = C;
+    static_assert(N * 8 <= (N / 2) * 80 && 2 * N * 4 <= (N / 2) * 80, "image / logs fit their regions");
 };
-
-// Twiddle (skew index) of tile group t of a 2^L-row transform at skew delta.
-template <int L> __device__ __forceinline__ uint32_t group_skew(uint32_t t, uint32_t delta) {
-    const int kb = L - 32 + __clz((uint32_t)((1 << L) - 1) - t);
-    const uint32_t j = t - ((1u << L) - (1u << (L - kb)));
-    return (j << (kb + 1)) + (1u << kb) + delta - 1u;
-}
 
 __device__ __forceinline__ void lds_table(uint32_t (&t)[20], const uint8_t* smem, uint32_t off) {
     const u32x4* p = (const u32x4*)(smem + off);
@@ -115,8 +114,59 @@ __device__ __forceinline__ void glb_table(uint32_t (&t)[20], const uint32_t* tab
 template <int L, bool FFT> __device__ __forceinline__ uint32_t tab_off(int kb, uint32_t r) {
     constexpr int N = 1 << L;
     const uint32_t t = (uint32_t)(N - (N >> kb)) + (r >> (kb + 1));
-    if (!FFT || kb == 0) return ColSmem<L>::A + t * 80u;
+    if (!FFT) return ColSmem<L>::A + t * 80u;
+    if (kb == 0) return ColSmem<L>::C + t * 80u;
     return ColSmem<L>::B + (t - N / 2) * 80u;
+}
+
+// LDS-DMA copy of `bytes` (a multiple of 16) from src to the LDS at dst by
+// all NT threads: instruction i of wave w moves bytes [(i NT + 64 w) 16, +1 KiB)
+// (the LDS destination of global_load_lds is the wave's base + 16 lane).
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef __attribute__((address_space(1))) const void* glb_vp;
+template <int NT>
+__device__ __forceinline__ void dma_copy(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
+    const uint32_t t = threadIdx.x, w = t >> 6;
+#pragma unroll
+    for (uint32_t i = 0; i * NT * 16 < bytes; i++) {
+        const uint32_t c = i * NT + t;
+        if (c * 16 < bytes)
+            __builtin_amdgcn_global_load_lds((glb_vp)(src + c * 16), (lds_vp)(dst + (i * NT + 64 * w) * 16), 16, 0, 0);
+    }
+}
+
+// Trade register bit RB (register pairs m, m | 2^RB) with lane bit LB of
+// the wave: afterwards register bit RB holds the row bit lane bit LB held,
+// and the other way round (lane with LB = 0 takes the partner's m into its
+// m | 2^RB, lane with LB = 1 the partner's m | 2^RB into its m).
+template <int RB, int LB> __device__ __forceinline__ void swap_bit(uint32_t (&X)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        if (m & (1 << RB)) continue;
+        const int m1 = m | (1 << RB);
+        if constexpr (LB == 4 || LB == 5) {
+            // v_permlane16_swap: odd 16-lane rows of the first operand <-> even
+            // rows of the second; v_permlane32_swap: upper 32 lanes <-> lower 32
+            const auto r = LB == 4 ? __builtin_amdgcn_permlane16_swap(X[m], X[m1], false, false)
+                                   : __builtin_amdgcn_permlane32_swap(X[m], X[m1], false, false);
+            X[m] = r[0];
+            X[m1] = r[1];
+        } else {
+            const bool hi = (threadIdx.x >> LB) & 1u;
+            const uint32_t u = (uint32_t)xshfl<(1 << LB)>((int)X[m]);   // partner's m
+            const uint32_t v = (uint32_t)xshfl<(1 << LB)>((int)X[m1]);  // partner's m | 2^RB
+            X[m1] = hi ? X[m1] : u;
+            X[m] = hi ? v : X[m];
+        }
+    }
+}
+// Block (B0, B1) -> block (C0, C1) inside the wave: register bits 0 / 1
+// trade places with the lane bits that hold row bits C0 / C1.
+template <int LB0, int LB1> __device__ __forceinline__ void wave_exchange(uint32_t (&XL)[4], uint32_t (&XH)[4]) {
+    swap_bit<0, LB0>(XL);
+    swap_bit<0, LB0>(XH);
+    swap_bit<1, LB1>(XL);
+    swap_bit<1, LB1>(XH);
 }
 
 // The twiddle tables of one block: the layers on row bits B0 (if D0) and B1
@@ -218,12 +268,109 @@ __device__ __forceinline__ void cstamp(const ColArgs& a, int i) {
 #endif
 }
 
-template <int L, bool DEC>
-__global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
+// ---------------------------------------------------------------------------
+// eval_poly inside the decoder (COL_DEC_EVAL, high rate, n = 2N <= 2048 work
+// rows).  The reference evaluates H(LogWalsh . H(e)) over 65536 points
+// (src/engine.rs:207-218; erasure vector from rate_high.rs:183-197).  With e
+// zero outside [0, n) and only outputs in [0, n) needed, that is the XOR
+// convolution out[i] = sum_j e[j] W[i ^ j], W = H(LogWalsh), i.e.
+// H_n(H_n(e) . V) with the constant V = n^-1 H_n(W[0, n)) (HostTables::col_v):
+// two n-point transforms per workgroup instead of a separate kernel.  Exact
+// integers (|H_n(e)| <= n, |H_n(Y)| <= n 65535), reduced mod 65535 (65535 and
+// 0 are the same log to every consumer, exp[65535] == exp[0]).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fold65535(uint32_t u) {
+    u = (u & 0xFFFFu) + (u >> 16);
+    return (u & 0xFFFFu) + (u >> 16);
+}
+__device__ __forceinline__ uint32_t mod65535(int v) { return fold65535((uint32_t)(v + 65535 * 4096)); }
+
+// In-place n-point integer FWHT of the workgroup's points p = t + NT j
+// (x[j] in thread t): register layers (bits of j), lane layers (shuffles),
+// wave layers through the LDS scratch `sx` (n ints).  Ends with a barrier
+// (sx free again).
+template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* sx) {
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (!(j & d)) {
+                const int u = x[j], v = x[j + d];
+                x[j] = u + v;
+                x[j + d] = u - v;
+            }
+#define RS16_LANE(D)                                              \
+    _Pragma("unroll") for (int j = 0; j < 8; j++) {               \
+        const int p = xshfl<(D)>(x[j]);                           \
+        x[j] = (lane & (D)) ? p - x[j] : x[j] + p;                \
+    }
+    RS16_LANE(1) RS16_LANE(2) RS16_LANE(4) RS16_LANE(8) RS16_LANE(16) RS16_LANE(32)
+#undef RS16_LANE
+    constexpr int NW = NT / 64;
+    if constexpr (NW > 1) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) sx[t + NT * j] = x[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            int acc = 0;
+#pragma unroll
+            for (int v = 0; v < NW; v++) {
+                const int y = sx[lane + 64 * v + NT * j];
+                acc += (__builtin_popcount(w & (uint32_t)v) & 1) ? -y : y;
+            }
+            x[j] = acc;
+        }
+        __syncthreads();
+    }
+}
+
+// The erasure logs of work rows [0, 2N) into elds, and the received counts
+// per 64-row chunk (rcount, workgroup 0) for rs16_decode_check.  Segment A =
+// recovery rows [0, in_rows) (flags), [in_rows, N) padding (erased), segment
+// B = originals [N, N + o_rows) (flags_o) (rate_high.rs:183-197).
+template <int L> __device__ __forceinline__ void col_eval(const ColArgs& a, uint32_t* elds) {
     constexpr int N = 1 << L, NT = N / 4;
-    constexpr int NTAB = N - 1;               // twiddle tables per direction
-    constexpr int CPL = (5 * NTAB + NT - 1) / NT;  // 16-byte table chunks per thread per direction (20)
-    constexpr int LATE = 5 * (N / 2) / NT;    // the FFT's layer-0 chunks: i < LATE (10)
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    uint8_t f[8];
+    uint32_t vt[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t p = t + NT * j;
+        const bool in_a = p < a.in_rows, in_b = p >= N && p - N < a.o_rows;
+        const uint8_t* fp = in_a && a.flags ? a.flags + p : (in_b && a.flags_o ? a.flags_o + (p - N) : a.zero);
+        f[j] = *(const __attribute__((address_space(1))) uint8_t*)fp;
+        vt[j] = a.vtab[p];
+    }
+    int x[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t p = t + NT * j;
+        const bool in_a = p < a.in_rows, in_b = p >= N && p - N < a.o_rows;
+        const bool rcv = in_a ? (!a.flags || f[j]) : (in_b && (!a.flags_o || f[j]));
+        x[j] = (in_a || in_b) ? !rcv : (p < N);
+        if (blockIdx.x == 0 && a.rcount) {
+            const uint64_t ra = __ballot(rcv && in_a), rb = __ballot(rcv && in_b);
+            if (lane == 0) {
+                a.rcount[2 * (p >> 6)] = (uint32_t)__popcll(ra);
+                a.rcount[2 * (p >> 6) + 1] = (uint32_t)__popcll(rb);
+            }
+        }
+    }
+    int* sx = (int*)elds;
+    fwht_points<NT>(x, sx);
+#pragma unroll
+    for (int j = 0; j < 8; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
+    fwht_points<NT>(x, sx);
+#pragma unroll
+    for (int j = 0; j < 8; j++) elds[t + NT * j] = mod65535(x[j]);
+}
+
+template <int L, int MODE>
+__global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
+    constexpr bool DEC = MODE != COL_ENC, EVAL = MODE == COL_DEC_EVAL;
+    constexpr int N = 1 << L, NT = N / 4;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t t = threadIdx.x;
     cstamp(a, 0);
@@ -238,7 +385,15 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     const uint8_t* in = a.in + st * a.bs_in + offL;
     uint8_t* out = a.out + st * a.bs_out + offL;
 
-    // ---- requests: rows, the decoder's erasure data, then the twiddle tables
+    // ---- requests: the tables (LDS-DMA), the rows, the decoder's erasure data
+    // (COL_DEC_EVAL: the tables after the polynomial, whose loads would wait
+    // behind them -- the compiler drains every LDS-DMA load at the first use
+    // of an ordinary load issued while one is in flight)
+    auto dma_tables = [&]() {
+        dma_copy<NT>(a.img_ifft, smem + ColSmem<L>::A, (N - 1) * 80);
+        dma_copy<NT>(a.img_fft + (N / 2) * 80, smem + ColSmem<L>::B, (N / 2 - 1) * 80);
+    };
+    if constexpr (!EVAL) dma_tables();
     uint32_t XL[4], XH[4];
 #pragma unroll
     for (int m = 0; m < 4; m++) {
@@ -249,43 +404,38 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         XL[m] = p[0];
         XH[m] = p[8];
     }
-    // decoder: eval_poly's output before its last 256-point FWHT (a.elog =
-    // the engine's ework): wave w finishes the blocks of rows [512 w, 512 w + 512)
-    uint32_t zv[2][4];
-    bool rcv[4] = {true, true, true, true};
+    uint32_t gt[DEC ? 4 : 1][20];
+    uint32_t ev[4] = {0, 0, 0, 0};
     if constexpr (DEC) {
-        const uint32_t w = t >> 6, lane = t & 63;
-#pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) zv[b][j] = a.elog[(2 * w + b) * 256 + lane + 64 * j];
+        bool rcv[4];
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             const uint32_t r = 4 * t + m;
             rcv[m] = r < a.in_rows && (!a.flags || a.flags[r] != 0);
         }
-    }
-    u32x4 s1[CPL], s2[CPL];
-    const u32x4* skew_tab = (const u32x4*)a.skew_tab;
-#pragma unroll
-    for (int i = 0; i < CPL; i++) {
-        const uint32_t c = t + (uint32_t)i * NT;
-        if (c < 5 * NTAB) s1[i] = skew_tab[(size_t)group_skew<L>(c / 5, a.skew_ifft) * (TAB_DWORDS / 4) + c % 5];
-    }
-    uint32_t gt[DEC ? 4 : 1][20];
-    uint32_t ev[4] = {0, 0, 0, 0};
-    if constexpr (DEC) {
-        // the last H_lo of eval_poly (src/engine.rs:207-218) for the work
-        // rows this codec reads: erasure logs of rows [0, 2^(L+1)) in LDS
         uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
-        const uint32_t w = t >> 6, lane = t & 63;
+        if constexpr (EVAL) {
+            col_eval<L>(a, elds);
+            __syncthreads();
+            dma_tables();
+        } else {
+            // eval_poly's output before its last 256-point FWHT (a.elog = the
+            // engine's ework): wave w finishes the blocks of rows [512 w, 512 w + 512)
+            // (src/engine.rs:207-218) into LDS, for the work rows this codec reads
+            uint32_t zv[2][4];
+            const uint32_t w = t >> 6, lane = t & 63;
 #pragma unroll
-        for (int b = 0; b < 2; b++) {
-            fwht256_wave(zv[b]);
+            for (int b = 0; b < 2; b++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) elds[(2 * w + b) * 256 + lane + 64 * j] = zv[b][j];
+                for (int j = 0; j < 4; j++) zv[b][j] = a.elog[(2 * w + b) * 256 + lane + 64 * j];
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                fwht256_wave(zv[b]);
+#pragma unroll
+                for (int j = 0; j < 4; j++) elds[(2 * w + b) * 256 + lane + 64 * j] = zv[b][j];
+            }
+            __syncthreads();
         }
-        __syncthreads();
         // gather multipliers: the v_perm table of each received row's log
         // (MULTIPLY SHARDS, rate_high.rs:203-228: other rows times zero)
 #pragma unroll
@@ -295,19 +445,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             ev[m] = elds[a.base_out + r];
         }
     }
-#pragma unroll
-    for (int i = 0; i < CPL; i++) {
-        const uint32_t c = t + (uint32_t)i * NT;
-        if (c < 5 * NTAB) s2[i] = skew_tab[(size_t)group_skew<L>(c / 5, a.skew_fft) * (TAB_DWORDS / 4) + c % 5];
-    }
-
     cstamp(a, 1);
-    // ---- stage the IFFT's tables into A (the FFT's after the first block)
-#pragma unroll
-    for (int i = 0; i < CPL; i++) {
-        const uint32_t c = t + (uint32_t)i * NT;
-        if (c < 5 * NTAB) *(u32x4*)(smem + ColSmem<L>::A + (c / 5) * 80 + (c % 5) * 16) = s1[i];
-    }
     if constexpr (DEC) {
 #pragma unroll
         for (int m = 0; m < 4; m++) {
@@ -317,37 +455,31 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             XH[m] = zh;
         }
     }
+    __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads have landed)
     __syncthreads();
     cstamp(a, 2);
-    // FFT tables, written between the barriers of the first exchange: layer 0
-    // over the IFFT's layer 0 (dead by then), layers >= 1 into B
-    auto stage_fft = [&]() {
-#pragma unroll
-        for (int i = 0; i < CPL; i++) {
-            const uint32_t c = t + (uint32_t)i * NT;
-            if (i < LATE) *(u32x4*)(smem + ColSmem<L>::A + (c / 5) * 80 + (c % 5) * 16) = s2[i];
-            else if (c < 5 * NTAB) *(u32x4*)(smem + ColSmem<L>::B + (c / 5 - N / 2) * 80 + (c % 5) * 16) = s2[i];
-        }
-    };
+    // the FFT's layer-0 tables into C (the decoder's logs there are read)
+    dma_copy<NT>(a.img_fft, smem + ColSmem<L>::C, (N / 2) * 80);
 
     // ---- IFFT (layers 0 .. L-1) then FFT (L-1 .. 0) in radix-4 blocks; the
-    // next block's tables are read before each exchange's barrier
+    // next block's tables are read before each exchange
     BlockTabs ta, tb;
     load_tabs<L, false, 0, 1, true, true>(ta, t, smem);
     compute<false, true, true>(XL, XH, ta);
     cstamp(a, 3);
     load_tabs<L, false, 2, 3, true, true>(tb, t, smem);
-    exchange<0, 1, 2, 3>(XL, XH, t, smem, stage_fft);
+    wave_exchange<0, 1>(XL, XH);
     compute<false, true, true>(XL, XH, tb);
     load_tabs<L, false, 4, 5, true, true>(ta, t, smem);
-    exchange<2, 3, 4, 5>(XL, XH, t, smem);
+    wave_exchange<2, 3>(XL, XH);
     compute<false, true, true>(XL, XH, ta);
     cstamp(a, 4);
     load_tabs<L, false, 6, 7, true, true>(tb, t, smem);
-    exchange<4, 5, 6, 7>(XL, XH, t, smem);
+    wave_exchange<4, 5>(XL, XH);
     compute<false, true, true>(XL, XH, tb);
     if constexpr (L == 10) {
         load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
+        __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
         exchange<6, 7, 8, 9>(XL, XH, t, smem);
         compute<false, true, true>(XL, XH, ta);
         cstamp(a, 5);
@@ -355,29 +487,32 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         load_tabs<L, true, 8, 9, true, true>(tb, t, smem);
         compute<true, true, true>(XL, XH, tb);
         load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
+        __syncthreads();  // (every wave has read its rows of the image)
         exchange<8, 9, 6, 7>(XL, XH, t, smem);
     } else {
         static_assert(L == 9, "the column codec covers 2^9 and 2^10 rows");
         load_tabs<L, false, 7, 8, false, true>(ta, t, smem);
+        __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
         exchange<6, 7, 7, 8>(XL, XH, t, smem);
         compute<false, false, true>(XL, XH, ta);
         cstamp(a, 5);
         load_tabs<L, true, 7, 8, false, true>(tb, t, smem);
         compute<true, false, true>(XL, XH, tb);
         load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
+        __syncthreads();  // (every wave has read its rows of the image)
         exchange<7, 8, 6, 7>(XL, XH, t, smem);
     }
     cstamp(a, 6);
     compute<true, true, true>(XL, XH, ta);
     load_tabs<L, true, 4, 5, true, true>(tb, t, smem);
-    exchange<6, 7, 4, 5>(XL, XH, t, smem);
+    wave_exchange<4, 5>(XL, XH);
     compute<true, true, true>(XL, XH, tb);
     cstamp(a, 7);
     load_tabs<L, true, 2, 3, true, true>(ta, t, smem);
-    exchange<4, 5, 2, 3>(XL, XH, t, smem);
+    wave_exchange<2, 3>(XL, XH);
     compute<true, true, true>(XL, XH, ta);
     load_tabs<L, true, 0, 1, true, true>(tb, t, smem);
-    exchange<2, 3, 0, 1>(XL, XH, t, smem);
+    wave_exchange<0, 1>(XL, XH);
     cstamp(a, 8);
     uint32_t rt[DEC ? 4 : 1][20];
     if constexpr (DEC) {
@@ -417,30 +552,21 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
 
 int col_rows_ok(uint32_t L) { return L == 9 || L == 10; }
 
-hipError_t launch_col(const ColArgs& a, uint32_t L, bool dec, hipStream_t s) {
-    if (!col_rows_ok(L)) return hipErrorInvalidValue;
+hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
+    if (!col_rows_ok(L) || mode < COL_ENC || mode > COL_DEC_EVAL) return hipErrorInvalidValue;
     if (a.qrow == 0 || a.nstripes == 0 || a.out_rows == 0) return hipSuccess;
-    const void* fn;
-    int lds;
-    if (L == 10) {
-        fn = dec ? (const void*)col_kernel<10, true> : (const void*)col_kernel<10, false>;
-        lds = ColSmem<10>::bytes(dec);
-    } else {
-        fn = dec ? (const void*)col_kernel<9, true> : (const void*)col_kernel<9, false>;
-        lds = ColSmem<9>::bytes(dec);
-    }
+    typedef void (*ColFn)(ColArgs);
+    static const ColFn fns[2][3] = {
+        {col_kernel<9, COL_ENC>, col_kernel<9, COL_DEC_EWORK>, col_kernel<9, COL_DEC_EVAL>},
+        {col_kernel<10, COL_ENC>, col_kernel<10, COL_DEC_EWORK>, col_kernel<10, COL_DEC_EVAL>},
+    };
+    const ColFn fn = fns[L - 9][mode];
+    const int lds = L == 10 ? ColSmem<10>::BYTES : ColSmem<9>::BYTES;
     if (lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
     }
-    dim3 grid(a.qrow * a.nstripes), block((1u << L) / 4);
-    if (L == 10) {
-        if (dec) hipLaunchKernelGGL((col_kernel<10, true>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((col_kernel<10, false>), grid, block, lds, s, a);
-    } else {
-        if (dec) hipLaunchKernelGGL((col_kernel<9, true>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((col_kernel<9, false>), grid, block, lds, s, a);
-    }
+    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3((1u << L) / 4), lds, s, a);
     return hipGetLastError();
 }
 

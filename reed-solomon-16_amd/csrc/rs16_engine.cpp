@@ -216,7 +216,8 @@ int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStr
 }
 
 bool rs16_engine::col_ok(int L, size_t S, size_t nstripes) const {
-    return col_rows_ok((uint32_t)L) && (S / 8) * nstripes <= col_max_quads && !(g_diag & DIAG_NO_COLUMN);
+    if (!col_rows_ok((uint32_t)L) || (g_diag & DIAG_NO_COLUMN)) return false;
+    return (S / 8) * nstripes <= col_max_quads || (g_diag & DIAG_FORCE_COLUMN);
 }
 
 ColArgs rs16_engine::col_args() const {
@@ -230,16 +231,24 @@ ColArgs rs16_engine::col_args() const {
     return a;
 }
 
-int rs16_engine::col(const ColArgs& a, int L, bool dec, hipStream_t s, rs16_error* err) {
+int rs16_engine::col(const ColArgs& args, int L, int mode, hipStream_t s, rs16_error* err) {
+    const bool dec = mode != COL_ENC;
+    // the table images of the two transforms (skew deltas 0 / 2^L only)
+    ColArgs a = args;
+    const uint32_t N = 1u << L;
+    if ((a.skew_ifft != 0 && a.skew_ifft != N) || (a.skew_fft != 0 && a.skew_fft != N))
+        return hip_fail(err, hipErrorInvalidValue);  // (unreachable: every caller passes 0 or 2^L)
+    a.img_ifft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_ifft ? 1 : 0));
+    a.img_fft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_fft ? 1 : 0));
     hipEvent_t ev;
     const int prof = dec ? PROF_COL_DEC : PROF_COL_ENC;
     if (int rc = prof_begin(s, &ev, err)) return rc;
     if (stamp_buf && stamp_prof == prof) {
         ColArgs b = a;
         b.stamps = (uint64_t*)stamp_buf;
-        RS16_HIP(launch_col(b, (uint32_t)L, dec, s));
+        RS16_HIP(launch_col(b, (uint32_t)L, mode, s));
     } else {
-        RS16_HIP(launch_col(a, (uint32_t)L, dec, s));
+        RS16_HIP(launch_col(a, (uint32_t)L, mode, s));
     }
     return prof_end(prof, s, ev, err);
 }
@@ -330,7 +339,7 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
         c.out_rows = (uint32_t)m;
         c.skew_ifft = (uint32_t)chunk;
         c.skew_fft = 0;
-        return col(c, L, false, s, err);
+        return col(c, L, COL_ENC, s, err);
     }
     // odd L: the extra row bit goes to the strided two-direction pass (an
     // 8 / 7 / 8 split measured 2-3 us slower per encode)
@@ -363,13 +372,13 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
 int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                               const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                               hipStream_t s, rs16_error* err) {
-    if (int rc = decode_eval(g, flags_a, flags_b, s, err)) return rc;
+    if (int rc = decode_eval(g, flags_a, flags_b, s, err, S)) return rc;
     return decode_passes(g, S, S_user, seg_a, flags_a, seg_b, flags_b, rest, Z, U, s, err);
 }
 
 // Erasure logs e = eval_poly(erasure vector) into ws_elog (2-3 small kernels).
 int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
-                             rs16_error* err) {
+                             rs16_error* err, size_t S, size_t nstripes) {
     RS16_HIP(ws_work32.reserve(GF_ORDER * 4));
     RS16_HIP(ws_elog.reserve(GF_ORDER * 4));
     RS16_HIP(ws_zflag.reserve(256));
@@ -400,6 +409,11 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.rcount = (uint32_t*)ws_rcount.p;
     last_dec = g;
     last_dec_valid = true;
+    // High-rate half decodes of 2^9 / 2^10-row halves through the column
+    // codec: it evaluates the polynomial itself (an n-point XOR convolution,
+    // rs16_col.hip) and writes rcount; no kernel here.
+    eval_in_col = S && g.high && half_decode(g) && col_ok(ilog2(g.n) - 1, S, nstripes);
+    if (eval_in_col) return RS16_OK;
     es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
     hipEvent_t ev;
     if (int rc = prof_begin(s, &ev, err)) return rc;
@@ -501,8 +515,16 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
             c.out_rows = orig;
             c.base_in = c.skew_ifft = src;
             c.base_out = c.skew_fft = dst;
+            if (eval_in_col && g.high) {
+                // eval_poly in the kernel (decode_eval launched nothing)
+                c.flags_o = flags_b;
+                c.o_rows = g.b_count;
+                c.vtab = d_col_v + col_v_offset(g.n);
+                c.rcount = (uint32_t*)ws_rcount.p;
+                return col(c, Lh, COL_DEC_EVAL, s, err);
+            }
             c.elog = (const uint32_t*)ws_work32.p;  // (eval_poly without its last H_lo: elog_fused)
-            return col(c, Lh, true, s, err);
+            return col(c, Lh, COL_DEC_EWORK, s, err);
         }
         const int lo = Lh / 2, hi = Lh - lo;
         a.lo = 0;
@@ -655,7 +677,7 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
         c.out_rows = (uint32_t)m;
         c.skew_ifft = 0;
         c.skew_fft = (uint32_t)chunk;
-        return col(c, L, false, s, err);
+        return col(c, L, COL_ENC, s, err);
     }
     RS16_HIP(ws_u.reserve(chunk * S));
     uint8_t* U = (uint8_t*)ws_u.p;

@@ -74,6 +74,8 @@ struct rs16_engine {
     hipStream_t stream = nullptr;
     uint32_t* d_skew_tab = nullptr;  // v_perm table per twiddle index (8 MiB)
     uint32_t* d_mul_tab = nullptr;
+    uint32_t* d_col_img = nullptr;   // column codec table images (HostTables::col_img)
+    uint32_t* d_col_v = nullptr;     // column codec eval_poly tables (HostTables::col_v)
     uint16_t* d_log_walsh = nullptr;
     uint8_t* d_zero_sink = nullptr;  // zero page + store sink (PassArgs::zero / sink)
     // scratch
@@ -152,6 +154,7 @@ struct rs16_engine {
     void* stamp_buf = nullptr;
     int stamp_prof = -1;
     bool elog_fused = false;  // last decode_eval left the final 256-point FWHT to the passes (ws_work32)
+    bool eval_in_col = false; // last decode_eval left eval_poly to the column codec (COL_DEC_EVAL)
     struct ProfRec {
         int id;
         hipEvent_t a, b;
@@ -180,8 +183,11 @@ struct rs16_engine {
                      const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                      hipStream_t s, rs16_error* err);
     // decode_fused = decode_eval (erasure logs into ws_elog) + decode_passes.
+    // S / nstripes: the width of the decode_passes launches that follow (0:
+    // unknown); when the column codec will run them as a high-rate half
+    // decode it computes eval_poly itself and no kernel is launched here.
     int decode_eval(const rs16::DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
-                    rs16_error* err);
+                    rs16_error* err, size_t S = 0, size_t nstripes = 1);
     int decode_passes(const rs16::DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                       const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                       hipStream_t s, rs16_error* err, size_t nstripes = 1, size_t bs_a = 0, size_t bs_b = 0,
@@ -193,9 +199,9 @@ struct rs16_engine {
     // used when the launch has at most col_max_quads quad columns (x
     // stripes); wider launches take the pass codec, whose tiles share each
     // twiddle table over 32 quad columns.
-    uint32_t col_max_quads = 1u << 30;
+    uint32_t col_max_quads = 256;  // (measured: scripts/probe_col.py)
     bool col_ok(int L, size_t S, size_t nstripes) const;
-    int col(const rs16::ColArgs& a, int L, bool dec, hipStream_t s, rs16_error* err);
+    int col(const rs16::ColArgs& a, int L, int mode, hipStream_t s, rs16_error* err);
     rs16::ColArgs col_args() const;
     // Multi-chunk encoders (high rate with k > chunk, low rate): every chunk's
     // transform in one batched set of launches.  d_orig rows have pitch

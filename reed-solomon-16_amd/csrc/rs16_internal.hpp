@@ -16,7 +16,20 @@ struct HostTables {
     std::vector<uint32_t> skew_entry;  // GF_ORDER entries: mul-table entry of each twiddle
     std::vector<uint32_t> mul_tab;     // TAB_ENTRIES * TAB_DWORDS
     std::vector<uint32_t> skew_tab;    // GF_ORDER * TAB_DWORDS: mul_tab row of skew_entry[i]
+    // Column codec (rs16_col.hip): the 2^L - 1 twiddle tables (20 dwords
+    // each, tile-group order) of a 2^L-row transform at skew delta 0 or 2^L,
+    // contiguous, for L = 9, 10; image (L, d) at col_img_offset(L, d) dwords.
+    std::vector<uint32_t> col_img;
+    // eval_poly of a high-rate decode with n <= 2048 work rows as an n-point
+    // XOR convolution (rs16_col.hip): col_v[off(n) + k] = n^-1 H_n(W)[k] mod
+    // 65535 with W = H_65536(log_walsh) (n = 2048 at 0, n = 1024 at 2048).
+    std::vector<uint32_t> col_v;
 };
+constexpr size_t col_v_offset(uint32_t n) { return n == 2048 ? 0 : 2048; }
+constexpr size_t col_img_offset(uint32_t L, uint32_t d) {
+    return L == 9 ? (size_t)d * 511 * 20 : 2 * 511 * 20 + (size_t)d * 1023 * 20;
+}
+constexpr size_t COL_IMG_DWORDS = 2 * 511 * 20 + 2 * 1023 * 20;
 const HostTables& host_tables();
 
 // ---------------------------------------------------------------------------
@@ -150,6 +163,15 @@ struct PassArgs {
 //        the 2^(L+1) work rows, whose last 256-point FWHT the kernel does
 //        itself: elog = eval_poly's output without it (the engine's ework)
 struct ColArgs {
+    const uint8_t* img_ifft;    // the transforms' table images (HostTables::col_img)
+    const uint8_t* img_fft;
+    // decoder computing eval_poly itself (high rate, COL_DEC_EVAL): the
+    // originals' received flags / count (segment B), HostTables::col_v of
+    // n = 2^(L+1), and the per-64-row received counts (ErasureSpec::rcount)
+    const uint8_t* flags_o;
+    uint32_t o_rows;
+    const uint32_t* vtab;
+    uint32_t* rcount;
     const uint8_t* in;
     const uint8_t* flags;
     uint8_t* out;
@@ -167,7 +189,8 @@ struct ColArgs {
     uint64_t* stamps;           // RS16_STAMPS builds: phase timeline (rs16_engine_set_stamps)
 };
 int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec covers
-hipError_t launch_col(const ColArgs& a, uint32_t L, bool dec, hipStream_t s);
+enum ColMode : int { COL_ENC = 0, COL_DEC_EWORK, COL_DEC_EVAL };
+hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s);
 
 // Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):
 // alternative code paths kept for tests and measurements, never needed for
@@ -177,6 +200,7 @@ enum DiagFlags : int {
     DIAG_EVAL_TWO_KERNEL = 2, // eval_poly: two-kernel form even when the one-kernel form applies
     DIAG_EVAL_FULL = 4,       // eval_poly: the full 65536-point form even for n <= 2048
     DIAG_NO_COLUMN = 8,       // 2^9 / 2^10-row transforms through the pass codec (rs16_col.hip off)
+    DIAG_FORCE_COLUMN = 16,   // ... through the column codec at any width (rs16_engine::col_max_quads ignored)
 };
 extern int g_diag;
 

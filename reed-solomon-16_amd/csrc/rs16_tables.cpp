@@ -127,6 +127,52 @@ void build(HostTables& t) {
     t.skew_tab.resize((size_t)GF_ORDER * TAB_DWORDS);
     for (uint32_t i = 0; i < GF_ORDER; i++)
         std::copy_n(&t.mul_tab[(size_t)t.skew_entry[i] * TAB_DWORDS], TAB_DWORDS, &t.skew_tab[(size_t)i * TAB_DWORDS]);
+
+    // Column codec images: table g of layer kb (g = 2^L - 2^(L-kb) + j, group
+    // j covering rows [j 2^(kb+1), (j+1) 2^(kb+1))) is the twiddle of skew
+    // index j 2^(kb+1) + 2^kb + delta - 1 (engine_naive.rs:43-124).
+    t.col_img.assign(COL_IMG_DWORDS, 0);
+    for (uint32_t L = 9; L <= 10; L++)
+        for (uint32_t d = 0; d < 2; d++) {
+            const uint32_t N = 1u << L, delta = d ? N : 0;
+            uint32_t* img = &t.col_img[col_img_offset(L, d)];
+            for (uint32_t g = 0; g + 1 < N; g++) {
+                uint32_t kb = 0;
+                while (g >= N - (N >> (kb + 1))) kb++;
+                const uint32_t j = g - (N - (N >> kb));
+                const uint32_t idx = (j << (kb + 1)) + (1u << kb) + delta - 1;
+                std::copy_n(&t.skew_tab[(size_t)idx * TAB_DWORDS], 20, img + (size_t)g * 20);
+            }
+        }
+
+    // eval_poly (src/engine.rs:207-218) = H(log_walsh . H(e)) over 65536
+    // points; for e supported on [0, n) and outputs on [0, n) it is the XOR
+    // convolution out[i] = sum_j e[j] W[i ^ j], W = H(log_walsh), i.e.
+    // H_n(H_n(e) . V) with V = n^-1 H_n(W[0, n)) (n^-1 = 2^(16 - log2 n)
+    // mod 65535).  Exact integers, reduced mod 65535.
+    {
+        std::vector<int64_t> w(GF_ORDER);
+        for (uint32_t i = 0; i < GF_ORDER; i++) w[i] = t.log_walsh[i];
+        auto fwht = [](int64_t* x, uint32_t n) {
+            for (uint32_t d = 1; d < n; d <<= 1)
+                for (uint32_t i = 0; i < n; i += 2 * d)
+                    for (uint32_t j = i; j < i + d; j++) {
+                        const int64_t a = x[j], b = x[j + d];
+                        x[j] = a + b;
+                        x[j + d] = a - b;
+                    }
+        };
+        auto mod = [](int64_t v) { return (uint32_t)(((v % 65535) + 65535) % 65535); };
+        fwht(w.data(), GF_ORDER);
+        t.col_v.assign(2048 + 1024, 0);
+        for (uint32_t n : {2048u, 1024u}) {
+            std::vector<int64_t> v(n);
+            for (uint32_t i = 0; i < n; i++) v[i] = mod(w[i]);
+            fwht(v.data(), n);
+            const int64_t inv = n == 2048 ? 32 : 64;  // 2^-11 / 2^-10 mod 65535 (2^16 = 1)
+            for (uint32_t k = 0; k < n; k++) t.col_v[col_v_offset(n) + k] = mod(mod(v[k]) * inv);
+        }
+    }
 }
 }  // namespace
 

@@ -59,7 +59,7 @@ def case(eng, k, m, S, nst, diag, n=200):
     eng.set_profiling(False)
     rs16.set_diagnostics(0)
     gib = (k + m) * S * nst / 2**30
-    print(json.dumps({"k": k, "m": m, "S": S, "stripes": nst, "column": diag == 0, "restored": ok,
+    print(json.dumps({"k": k, "m": m, "S": S, "stripes": nst, "column": diag == rs16.DIAG_FORCE_COLUMN, "restored": ok,
                       "encode_us": round(te, 2), "decode_us": round(td, 2),
                       "encode_gib_s": round(gib / te * 1e6, 1), "decode_gib_s": round(gib / td * 1e6, 1),
                       "kernels_us": prof}), flush=True)
@@ -67,10 +67,10 @@ def case(eng, k, m, S, nst, diag, n=200):
 
 def main():
     eng = rs16.default_engine()
-    for (k, m, S, nst) in [(1000, 1000, 1024, 1), (512, 512, 1024, 1), (1000, 1000, 4096, 1),
-                           (1000, 1000, 16384, 1), (1000, 1000, 65536, 1), (1000, 1000, 1024, 32),
-                           (1000, 1000, 1024, 8)]:
-        for diag in (0, rs16.DIAG_NO_COLUMN):
+    for (k, m, S, nst) in [(1000, 1000, 1024, 1), (512, 512, 1024, 1), (1000, 1000, 2048, 1),
+                           (1000, 1000, 4096, 1), (1000, 1000, 1024, 2), (1000, 1000, 1024, 4),
+                           (1000, 1000, 16384, 1), (1000, 1000, 1024, 32)]:
+        for diag in (rs16.DIAG_FORCE_COLUMN, rs16.DIAG_NO_COLUMN):
             case(eng, k, m, S, nst, diag)
 
 

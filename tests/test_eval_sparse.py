@@ -73,3 +73,43 @@ def test_fused_eval_formulation_matches_oracle(seed):
     want = e.copy()
     O.eval_poly(want, 65536)
     assert np.array_equal(got % 65535, want.astype(np.int64) % 65535)
+
+
+def _fwht_int(x):
+    x = x.astype(np.int64).copy()
+    n = x.size
+    d = 1
+    while d < n:
+        x = x.reshape(-1, 2, d)
+        a, b = x[:, 0, :].copy(), x[:, 1, :].copy()
+        x[:, 0, :], x[:, 1, :] = a + b, a - b
+        x = x.reshape(-1)
+        d *= 2
+    return x
+
+
+def conv_eval(e, n):
+    """The column codec's eval_poly (rs16_col.hip col_eval; V built like
+    rs16_tables.cpp col_v): for e zero outside [0, n), rows [0, n) of
+    H(LogWalsh . H(e)) are the XOR convolution e (*) W, W = H(LogWalsh):
+    H_n(H_n(e) . V), V = n^-1 H_n(W[0, n)) mod 65535, n^-1 = 2^(16 - log2 n)."""
+    w = _fwht_int(O.table("log_walsh")) % 65535
+    inv = {2048: 32, 1024: 64}[n]
+    v = (_fwht_int(w[:n]) % 65535) * inv % 65535
+    x = _fwht_int(e[:n]) % 65535
+    return _fwht_int((x * v) % 65535) % 65535
+
+
+@pytest.mark.parametrize("n", [1024, 2048])
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_conv_eval_matches_oracle(n, seed):
+    rng = np.random.default_rng(seed * 7 + n)
+    e = np.zeros(65536, np.uint16)
+    e[:n] = rng.integers(0, 2, n) if seed else 0
+    e[n // 2 - 24: n // 2] = 1  # the padding rows [m, chunk) of a high-rate decode
+    if seed == 0:
+        e[n // 2:] = 0
+        e[n // 2: n // 2 + 1000 * n // 2048] = 1  # 100 % original loss
+    want = e.copy()
+    O.eval_poly(want, n)
+    assert np.array_equal(conv_eval(e, n), want[:n].astype(np.int64) % 65535)

@@ -24,6 +24,13 @@ def eng():
 
 
 @pytest.fixture
+def force_column():
+    old = rs16.set_diagnostics(rs16.DIAG_FORCE_COLUMN)
+    yield
+    rs16.set_diagnostics(old)
+
+
+@pytest.fixture
 def no_column():
     old = rs16.set_diagnostics(rs16.DIAG_NO_COLUMN)
     yield
@@ -66,10 +73,14 @@ def test_col_encode_vs_oracle(eng, k, m, sb):
 
 
 @pytest.mark.parametrize("sb", [192, 4096, 65536])
-def test_col_encode_widths(eng, sb):
+def test_col_encode_widths(eng, sb, force_column):
+    # (wider than the codec's default limit: forced, rs16.DIAG_FORCE_COLUMN)
     k, m = 1000, 1000
     original = generate_original(k, sb, sb)
-    assert np.array_equal(dev_encode(eng, original, m), O.encode(k, m, original))
+    recovery = dev_encode(eng, original, m)
+    assert np.array_equal(recovery, O.encode(k, m, original))
+    om, rm = np.zeros(k, bool), np.ones(m, bool)
+    assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
 
 
 @pytest.mark.parametrize("k,m", [(1000, 1000), (300, 1000), (512, 512), (1024, 600)])
@@ -134,9 +145,10 @@ def test_col_rate_api_in_place(eng, rate, k, m):
     assert all(np.array_equal(np.frombuffer(got[i], np.uint8), original[i]) for i in range(lost))
 
 
-@pytest.mark.parametrize("k,m,n", [(1000, 1000, 5), (512, 512, 3), (300, 1000, 4)])
-def test_col_batched_stripes(eng, k, m, n):
-    sb, pad = 128, 64
+@pytest.mark.parametrize("k,m,n,sb", [(1000, 1000, 5, 128), (512, 512, 3, 128), (300, 1000, 4, 128),
+                                      (1000, 1000, 6, 1024)])
+def test_col_batched_stripes(eng, k, m, n, sb, force_column):
+    pad = 64
     so, sr = k * sb + pad, m * sb + pad
     stripes = [generate_original(k, sb, 11 * i + k) for i in range(n)]
     host_o = np.full(n * so, 0xEE, np.uint8)
@@ -183,3 +195,21 @@ def test_col_host_multi(eng):
     rec = np.zeros((m, sb), np.uint8)
     rs16.encode_host_multi(k, m, sb, original, rec, [eng, rs16.Engine(0)])
     assert np.array_equal(rec, O.encode(k, m, original))
+
+
+def test_col_decode_check_counts(eng):
+    """The column decoder evaluates the polynomial itself (no eval kernel) and
+    writes the per-chunk received counts rs16_decode_check reads: a caller
+    whose counts disagree with its flags gets InvalidArgument."""
+    k, m, sb = 900, 1000, 64
+    original = generate_original(k, sb, 5)
+    recovery = O.encode(k, m, original)
+    d_orig = DeviceArray.from_numpy(eng, np.zeros_like(original))
+    d_rec = DeviceArray.from_numpy(eng, recovery)
+    d_of = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+    d_rf = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+    rs16.decode_device(k, m, sb, d_orig.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, 0, m, engine=eng, check=True)
+    assert np.array_equal(d_orig.download(shape=(k, sb)), original)
+    with pytest.raises(rs16.Error) as e:
+        rs16.decode_device(k, m, sb, d_orig.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, 0, m - 1, engine=eng, check=True)
+    assert e.value.kind == "InvalidArgument"
