@@ -305,8 +305,26 @@ template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* 
         const int p = xshfl<(D)>(x[j]);                           \
         x[j] = (lane & (D)) ? p - x[j] : x[j] + p;                \
     }
-    RS16_LANE(1) RS16_LANE(2) RS16_LANE(4) RS16_LANE(8) RS16_LANE(16) RS16_LANE(32)
+    RS16_LANE(1) RS16_LANE(2) RS16_LANE(4) RS16_LANE(8)
 #undef RS16_LANE
+    // lane bits 4 and 5: trade places with register bit 0 (v_permlane16_swap /
+    // v_permlane32_swap, no LDS), butterfly the register pairs, trade back
+#pragma unroll
+    for (int lb = 4; lb <= 5; lb++)
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            auto sw = [&]() {
+                const auto r = lb == 4 ? __builtin_amdgcn_permlane16_swap((uint32_t)x[j], (uint32_t)x[j + 1], false, false)
+                                       : __builtin_amdgcn_permlane32_swap((uint32_t)x[j], (uint32_t)x[j + 1], false, false);
+                x[j] = (int)r[0];
+                x[j + 1] = (int)r[1];
+            };
+            sw();
+            const int u = x[j], v = x[j + 1];
+            x[j] = u + v;
+            x[j + 1] = u - v;
+            sw();
+        }
     constexpr int NW = NT / 64;
     if constexpr (NW > 1) {
 #pragma unroll
@@ -385,15 +403,14 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     const uint8_t* in = a.in + st * a.bs_in + offL;
     uint8_t* out = a.out + st * a.bs_out + offL;
 
-    // ---- requests: the tables (LDS-DMA), the rows, the decoder's erasure data
-    // (COL_DEC_EVAL: the tables after the polynomial, whose loads would wait
-    // behind them -- the compiler drains every LDS-DMA load at the first use
-    // of an ordinary load issued while one is in flight)
+    // ---- requests: the rows, the tables (LDS-DMA), the decoder's erasure data
+    // (the compiler drains every LDS-DMA load at the first use of an ordinary
+    // load while one is in flight: the decoder's polynomial starts once the
+    // tables are in)
     auto dma_tables = [&]() {
         dma_copy<NT>(a.img_ifft, smem + ColSmem<L>::A, (N - 1) * 80);
         dma_copy<NT>(a.img_fft + (N / 2) * 80, smem + ColSmem<L>::B, (N / 2 - 1) * 80);
     };
-    if constexpr (!EVAL) dma_tables();
     uint32_t XL[4], XH[4];
 #pragma unroll
     for (int m = 0; m < 4; m++) {
@@ -404,6 +421,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         XL[m] = p[0];
         XH[m] = p[8];
     }
+    dma_tables();
     uint32_t gt[DEC ? 4 : 1][20];
     uint32_t ev[4] = {0, 0, 0, 0};
     if constexpr (DEC) {
@@ -417,7 +435,6 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         if constexpr (EVAL) {
             col_eval<L>(a, elds);
             __syncthreads();
-            dma_tables();
         } else {
             // eval_poly's output before its last 256-point FWHT (a.elog = the
             // engine's ework): wave w finishes the blocks of rows [512 w, 512 w + 512)
