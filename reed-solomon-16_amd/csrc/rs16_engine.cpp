@@ -231,8 +231,33 @@ ColArgs rs16_engine::col_args() const {
     return a;
 }
 
+// The column codec's tables (HostTables::col_img / col_v), uploaded on the
+// engine's first column launch: engines that never run it allocate nothing.
+int rs16_engine::col_tables(hipStream_t s, rs16_error* err) {
+    if (d_col_img) return RS16_OK;
+    const HostTables& t = host_tables();
+    uint32_t *img = nullptr, *v = nullptr;
+    RS16_HIP(hipMalloc(&img, COL_IMG_DWORDS * 4));
+    if (hipError_t e = hipMalloc(&v, t.col_v.size() * 4)) {
+        (void)hipFree(img);
+        return hip_fail(err, e);
+    }
+    hipError_t e = hipMemcpyAsync(img, t.col_img.data(), COL_IMG_DWORDS * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(v, t.col_v.data(), t.col_v.size() * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // (pageable sources: keep no pending copy)
+    if (e != hipSuccess) {
+        (void)hipFree(img);
+        (void)hipFree(v);
+        return hip_fail(err, e);
+    }
+    d_col_img = img;
+    d_col_v = v;
+    return RS16_OK;
+}
+
 int rs16_engine::col(const ColArgs& args, int L, int mode, hipStream_t s, rs16_error* err) {
     const bool dec = mode != COL_ENC;
+    if (int rc = col_tables(s, err)) return rc;
     // the table images of the two transforms (skew deltas 0 / 2^L only)
     ColArgs a = args;
     const uint32_t N = 1u << L;
@@ -240,6 +265,7 @@ int rs16_engine::col(const ColArgs& args, int L, int mode, hipStream_t s, rs16_e
         return hip_fail(err, hipErrorInvalidValue);  // (unreachable: every caller passes 0 or 2^L)
     a.img_ifft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_ifft ? 1 : 0));
     a.img_fft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_fft ? 1 : 0));
+    if (mode == COL_DEC_EVAL) a.vtab = d_col_v + col_v_offset(2u << L);
     hipEvent_t ev;
     const int prof = dec ? PROF_COL_DEC : PROF_COL_ENC;
     if (int rc = prof_begin(s, &ev, err)) return rc;
@@ -519,7 +545,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
                 // eval_poly in the kernel (decode_eval launched nothing)
                 c.flags_o = flags_b;
                 c.o_rows = g.b_count;
-                c.vtab = d_col_v + col_v_offset(g.n);
+                c.vtab = nullptr;  // (col(): d_col_v + col_v_offset(2^(L+1)))
                 c.rcount = (uint32_t*)ws_rcount.p;
                 return col(c, Lh, COL_DEC_EVAL, s, err);
             }

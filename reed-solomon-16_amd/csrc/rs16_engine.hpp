@@ -202,6 +202,7 @@ struct rs16_engine {
     uint32_t col_max_quads = 256;  // (measured: scripts/probe_col.py)
     bool col_ok(int L, size_t S, size_t nstripes) const;
     int col(const rs16::ColArgs& a, int L, int mode, hipStream_t s, rs16_error* err);
+    int col_tables(hipStream_t s, rs16_error* err);
     rs16::ColArgs col_args() const;
     // Multi-chunk encoders (high rate with k > chunk, low rate): every chunk's
     // transform in one batched set of launches.  d_orig rows have pitch
