@@ -496,6 +496,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     compute<false, true, true>(XL, XH, tb);
     if constexpr (L == 10) {
         load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
+        __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
         __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
         exchange<6, 7, 8, 9>(XL, XH, t, smem);
         compute<false, true, true>(XL, XH, ta);
@@ -509,6 +510,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     } else {
         static_assert(L == 9, "the column codec covers 2^9 and 2^10 rows");
         load_tabs<L, false, 7, 8, false, true>(ta, t, smem);
+        __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
         __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
         exchange<6, 7, 7, 8>(XL, XH, t, smem);
         compute<false, false, true>(XL, XH, ta);
