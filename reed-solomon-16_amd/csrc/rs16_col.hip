@@ -85,6 +85,7 @@ template <int L> struct ColSmem {
     static constexpr int IMG = A;
     static constexpr int ELOG = C;
     static_assert(N * 8 <= (N / 2) * 80 && 2 * N * 4 <= (N / 2) * 80, "image / logs fit their regions");
+    static_assert(L >= (int)COL_LMIN && L <= (int)COL_LMAX, "the column codec covers 2^6 .. 2^10 rows");
 };
 
 __device__ __forceinline__ void lds_table(uint32_t (&t)[20], const uint8_t* smem, uint32_t off) {
@@ -301,16 +302,18 @@ template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* 
                 x[j + d] = u - v;
             }
 #define RS16_LANE(D)                                              \
-    _Pragma("unroll") for (int j = 0; j < 8; j++) {               \
-        const int p = xshfl<(D)>(x[j]);                           \
-        x[j] = (lane & (D)) ? p - x[j] : x[j] + p;                \
+    if constexpr ((D) < NT) {                                     \
+        _Pragma("unroll") for (int j = 0; j < 8; j++) {           \
+            const int p = xshfl<(D)>(x[j]);                       \
+            x[j] = (lane & (D)) ? p - x[j] : x[j] + p;            \
+        }                                                         \
     }
     RS16_LANE(1) RS16_LANE(2) RS16_LANE(4) RS16_LANE(8)
 #undef RS16_LANE
     // lane bits 4 and 5: trade places with register bit 0 (v_permlane16_swap /
     // v_permlane32_swap, no LDS), butterfly the register pairs, trade back
 #pragma unroll
-    for (int lb = 4; lb <= 5; lb++)
+    for (int lb = 4; lb <= 5 && (1 << lb) < NT; lb++)
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
             auto sw = [&]() {
@@ -362,6 +365,7 @@ template <int L> __device__ __forceinline__ void col_eval(const ColArgs& a, uint
         vt[j] = a.vtab[p];
     }
     int x[8];
+    uint32_t ca = 0, cb = 0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint32_t p = t + NT * j;
@@ -369,10 +373,16 @@ template <int L> __device__ __forceinline__ void col_eval(const ColArgs& a, uint
         const bool rcv = in_a ? (!a.flags || f[j]) : (in_b && (!a.flags_o || f[j]));
         x[j] = (in_a || in_b) ? !rcv : (p < N);
         if (blockIdx.x == 0 && a.rcount) {
-            const uint64_t ra = __ballot(rcv && in_a), rb = __ballot(rcv && in_b);
-            if (lane == 0) {
-                a.rcount[2 * (p >> 6)] = (uint32_t)__popcll(ra);
-                a.rcount[2 * (p >> 6) + 1] = (uint32_t)__popcll(rb);
+            // (below 64 threads a 64-row chunk spans 64 / NT values of j)
+            constexpr int PER = NT >= 64 ? 1 : 64 / NT;
+            ca += (uint32_t)__popcll(__ballot(rcv && in_a));
+            cb += (uint32_t)__popcll(__ballot(rcv && in_b));
+            if ((j + 1) % PER == 0) {
+                if (lane == 0) {
+                    a.rcount[2 * (p >> 6)] = ca;
+                    a.rcount[2 * (p >> 6) + 1] = cb;
+                }
+                ca = cb = 0;
             }
         }
     }
@@ -435,7 +445,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         if constexpr (EVAL) {
             col_eval<L>(a, elds);
             __syncthreads();
-        } else {
+        } else if constexpr (L >= 9) {
             // eval_poly's output before its last 256-point FWHT (a.elog = the
             // engine's ework): wave w finishes the blocks of rows [512 w, 512 w + 512)
             // (src/engine.rs:207-218) into LDS, for the work rows this codec reads
@@ -479,7 +489,10 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     dma_copy<NT>(a.img_fft, smem + ColSmem<L>::C, (N / 2) * 80);
 
     // ---- IFFT (layers 0 .. L-1) then FFT (L-1 .. 0) in radix-4 blocks; the
-    // next block's tables are read before each exchange
+    // next block's tables are read before each exchange.  Row bits 0-5 are
+    // lane bits of some block (in-wave exchanges); from L = 9 on the top ones
+    // are wave bits (two LDS exchanges); L = 7 ends with a one-layer block on
+    // bits (4, 6).
     BlockTabs ta, tb;
     load_tabs<L, false, 0, 1, true, true>(ta, t, smem);
     compute<false, true, true>(XL, XH, ta);
@@ -491,45 +504,72 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     wave_exchange<2, 3>(XL, XH);
     compute<false, true, true>(XL, XH, ta);
     cstamp(a, 4);
-    load_tabs<L, false, 6, 7, true, true>(tb, t, smem);
-    wave_exchange<4, 5>(XL, XH);
-    compute<false, true, true>(XL, XH, tb);
-    if constexpr (L == 10) {
-        load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
-        __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
-        __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
-        exchange<6, 7, 8, 9>(XL, XH, t, smem);
-        compute<false, true, true>(XL, XH, ta);
+    if constexpr (L == 6) {
+        // the FFT's first block keeps the row bits (4, 5)
         cstamp(a, 5);
-        // the FFT's first block keeps the row bits: no exchange
-        load_tabs<L, true, 8, 9, true, true>(tb, t, smem);
-        compute<true, true, true>(XL, XH, tb);
-        load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
-        __syncthreads();  // (every wave has read its rows of the image)
-        exchange<8, 9, 6, 7>(XL, XH, t, smem);
-    } else {
-        static_assert(L == 9, "the column codec covers 2^9 and 2^10 rows");
-        load_tabs<L, false, 7, 8, false, true>(ta, t, smem);
-        __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
-        __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
-        exchange<6, 7, 7, 8>(XL, XH, t, smem);
-        compute<false, false, true>(XL, XH, ta);
+        load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
+        cstamp(a, 6);
+    } else if constexpr (L == 7) {
+        load_tabs<L, false, 4, 6, false, true>(tb, t, smem);
+        swap_bit<1, 4>(XL);  // register bit 1: row bit 5 -> 6
+        swap_bit<1, 4>(XH);
+        compute<false, false, true>(XL, XH, tb);
         cstamp(a, 5);
-        load_tabs<L, true, 7, 8, false, true>(tb, t, smem);
+        load_tabs<L, true, 4, 6, false, true>(tb, t, smem);
         compute<true, false, true>(XL, XH, tb);
-        load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
-        __syncthreads();  // (every wave has read its rows of the image)
-        exchange<7, 8, 6, 7>(XL, XH, t, smem);
+        load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
+        swap_bit<1, 4>(XL);
+        swap_bit<1, 4>(XH);
+        cstamp(a, 6);
+    } else {
+        load_tabs<L, false, 6, 7, true, true>(tb, t, smem);
+        wave_exchange<4, 5>(XL, XH);
+        compute<false, true, true>(XL, XH, tb);
+        if constexpr (L == 8) {
+            cstamp(a, 5);
+            load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
+        } else if constexpr (L == 10) {
+            load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
+            __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
+            __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
+            exchange<6, 7, 8, 9>(XL, XH, t, smem);
+            compute<false, true, true>(XL, XH, ta);
+            cstamp(a, 5);
+            // the FFT's first block keeps the row bits: no exchange
+            load_tabs<L, true, 8, 9, true, true>(tb, t, smem);
+            compute<true, true, true>(XL, XH, tb);
+            load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
+            __syncthreads();  // (every wave has read its rows of the image)
+            exchange<8, 9, 6, 7>(XL, XH, t, smem);
+        } else {
+            load_tabs<L, false, 7, 8, false, true>(ta, t, smem);
+            __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
+            __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
+            exchange<6, 7, 7, 8>(XL, XH, t, smem);
+            compute<false, false, true>(XL, XH, ta);
+            cstamp(a, 5);
+            load_tabs<L, true, 7, 8, false, true>(tb, t, smem);
+            compute<true, false, true>(XL, XH, tb);
+            load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
+            __syncthreads();  // (every wave has read its rows of the image)
+            exchange<7, 8, 6, 7>(XL, XH, t, smem);
+        }
+        cstamp(a, 6);
+        compute<true, true, true>(XL, XH, ta);
+        load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
+        wave_exchange<4, 5>(XL, XH);
     }
-    cstamp(a, 6);
     compute<true, true, true>(XL, XH, ta);
-    load_tabs<L, true, 4, 5, true, true>(tb, t, smem);
-    wave_exchange<4, 5>(XL, XH);
-    compute<true, true, true>(XL, XH, tb);
     cstamp(a, 7);
-    load_tabs<L, true, 2, 3, true, true>(ta, t, smem);
+    load_tabs<L, true, 2, 3, true, true>(tb, t, smem);
     wave_exchange<2, 3>(XL, XH);
-    compute<true, true, true>(XL, XH, ta);
+    compute<true, true, true>(XL, XH, tb);
+    if constexpr (L <= 8) {
+        // (no barrier since the staging one: the FFT's layer-0 tables in C
+        // must have landed and be visible before the last block reads them)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
     load_tabs<L, true, 0, 1, true, true>(tb, t, smem);
     wave_exchange<0, 1>(XL, XH);
     cstamp(a, 8);
@@ -569,23 +609,27 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
 
 }  // namespace
 
-int col_rows_ok(uint32_t L) { return L == 9 || L == 10; }
+int col_rows_ok(uint32_t L) { return L >= COL_LMIN && L <= COL_LMAX; }
 
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
     if (!col_rows_ok(L) || mode < COL_ENC || mode > COL_DEC_EVAL) return hipErrorInvalidValue;
     if (a.qrow == 0 || a.nstripes == 0 || a.out_rows == 0) return hipSuccess;
     typedef void (*ColFn)(ColArgs);
-    static const ColFn fns[2][3] = {
-        {col_kernel<9, COL_ENC>, col_kernel<9, COL_DEC_EWORK>, col_kernel<9, COL_DEC_EVAL>},
-        {col_kernel<10, COL_ENC>, col_kernel<10, COL_DEC_EWORK>, col_kernel<10, COL_DEC_EVAL>},
-    };
-    const ColFn fn = fns[L - 9][mode];
-    const int lds = L == 10 ? ColSmem<10>::BYTES : ColSmem<9>::BYTES;
-    if (lds > 65536) {
-        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+#define RS16_COL_ROW(L) \
+    {col_kernel<L, COL_ENC>, L >= 9 ? col_kernel<L, COL_DEC_EWORK> : nullptr, col_kernel<L, COL_DEC_EVAL>}
+    static const ColFn fns[5][3] = {RS16_COL_ROW(6), RS16_COL_ROW(7), RS16_COL_ROW(8), RS16_COL_ROW(9),
+                                    RS16_COL_ROW(10)};
+#undef RS16_COL_ROW
+    static const int lds[5] = {ColSmem<6>::BYTES, ColSmem<7>::BYTES, ColSmem<8>::BYTES, ColSmem<9>::BYTES,
+                               ColSmem<10>::BYTES};
+    const ColFn fn = fns[L - COL_LMIN][mode];
+    if (!fn) return hipErrorInvalidValue;  // (the ework decoder needs 4 waves: L >= 9)
+    const int bytes = lds[L - COL_LMIN];
+    if (bytes > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3((1u << L) / 4), lds, s, a);
+    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3((1u << L) / 4), bytes, s, a);
     return hipGetLastError();
 }
 

@@ -345,12 +345,6 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
         a.bs_seg = bs_seg;
         return tiles * ns;
     };
-    if (L <= 8) {
-        a.out = d_rec;
-        a.S_out = S_user;
-        RS16_PASS(ENC_SINGLE, L, a, batch(1, 0, bs_rec, bs_orig), s);
-        return RS16_OK;
-    }
     if (col_ok(L, S, nst)) {
         // 512 / 1024-row chunks: the whole encode in one launch (rs16_col.hip)
         ColArgs c = col_args();
@@ -366,6 +360,12 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
         c.skew_ifft = (uint32_t)chunk;
         c.skew_fft = 0;
         return col(c, L, COL_ENC, s, err);
+    }
+    if (L <= 8) {
+        a.out = d_rec;
+        a.S_out = S_user;
+        RS16_PASS(ENC_SINGLE, L, a, batch(1, 0, bs_rec, bs_orig), s);
+        return RS16_OK;
     }
     // odd L: the extra row bit goes to the strided two-direction pass (an
     // 8 / 7 / 8 split measured 2-3 us slower per encode)
@@ -521,13 +521,16 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         a.row_base_in = a.skew_ifft = src;
         a.row_base_out = a.skew_fft = dst;
         const int Lh = L - 1;
-        if (Lh <= 8) {
+        // 2^6 .. 2^10-row halves: the whole decode in one launch (rs16_col.hip)
+        // -- high rate with the polynomial in the kernel; the low rate from
+        // 2^9 rows on, on eval_poly's output
+        const bool col_eval = eval_in_col && g.high;
+        if (!col_eval && Lh <= 8) {
             a.ework = nullptr;  // (decode_eval did the whole eval_poly)
             RS16_PASS(DEC_HALF_SINGLE, Lh, a, batch(1, 0, 0, 0), s);
             return RS16_OK;
         }
-        if (col_ok(Lh, S, ns)) {
-            // 512 / 1024-row halves: the whole decode in one launch (rs16_col.hip)
+        if (col_eval || col_ok(Lh, S, ns)) {
             ColArgs c = col_args();
             c.in = g.high ? seg_a : seg_b;
             c.flags = g.high ? flags_a : flags_b;
@@ -541,7 +544,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
             c.out_rows = orig;
             c.base_in = c.skew_ifft = src;
             c.base_out = c.skew_fft = dst;
-            if (eval_in_col && g.high) {
+            if (col_eval) {
                 // eval_poly in the kernel (decode_eval launched nothing)
                 c.flags_o = flags_b;
                 c.o_rows = g.b_count;

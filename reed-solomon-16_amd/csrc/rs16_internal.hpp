@@ -18,18 +18,24 @@ struct HostTables {
     std::vector<uint32_t> skew_tab;    // GF_ORDER * TAB_DWORDS: mul_tab row of skew_entry[i]
     // Column codec (rs16_col.hip): the 2^L - 1 twiddle tables (20 dwords
     // each, tile-group order) of a 2^L-row transform at skew delta 0 or 2^L,
-    // contiguous, for L = 9, 10; image (L, d) at col_img_offset(L, d) dwords.
+    // contiguous, for L = COL_LMIN .. COL_LMAX; image (L, d) at
+    // col_img_offset(L, d) dwords.
     std::vector<uint32_t> col_img;
-    // eval_poly of a high-rate decode with n <= 2048 work rows as an n-point
-    // XOR convolution (rs16_col.hip): col_v[off(n) + k] = n^-1 H_n(W)[k] mod
-    // 65535 with W = H_65536(log_walsh) (n = 2048 at 0, n = 1024 at 2048).
+    // eval_poly of a high-rate decode with n = 2^(L+1) <= 2048 work rows as
+    // an n-point XOR convolution (rs16_col.hip): col_v[col_v_offset(n) + k] =
+    // n^-1 H_n(W)[k] mod 65535 with W = H_65536(log_walsh).
     std::vector<uint32_t> col_v;
 };
-constexpr size_t col_v_offset(uint32_t n) { return n == 2048 ? 0 : 2048; }
+constexpr uint32_t COL_LMIN = 6, COL_LMAX = 10;
 constexpr size_t col_img_offset(uint32_t L, uint32_t d) {
-    return L == 9 ? (size_t)d * 511 * 20 : 2 * 511 * 20 + (size_t)d * 1023 * 20;
+    size_t off = 0;
+    for (uint32_t l = COL_LMIN; l < L; l++) off += 2 * ((1u << l) - 1) * 20;
+    return off + (size_t)d * ((1u << L) - 1) * 20;
 }
-constexpr size_t COL_IMG_DWORDS = 2 * 511 * 20 + 2 * 1023 * 20;
+constexpr size_t COL_IMG_DWORDS = col_img_offset(COL_LMAX + 1, 0);
+// n = 2^(COL_LMIN+1) .. 2^(COL_LMAX+1): tables of n entries at n - 2^(COL_LMIN+1)
+constexpr size_t col_v_offset(uint32_t n) { return n - (2u << COL_LMIN); }
+constexpr size_t COL_V_DWORDS = col_v_offset(4u << COL_LMAX);
 const HostTables& host_tables();
 
 // ---------------------------------------------------------------------------

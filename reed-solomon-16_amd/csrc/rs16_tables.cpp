@@ -132,7 +132,7 @@ void build(HostTables& t) {
     // j covering rows [j 2^(kb+1), (j+1) 2^(kb+1))) is the twiddle of skew
     // index j 2^(kb+1) + 2^kb + delta - 1 (engine_naive.rs:43-124).
     t.col_img.assign(COL_IMG_DWORDS, 0);
-    for (uint32_t L = 9; L <= 10; L++)
+    for (uint32_t L = COL_LMIN; L <= COL_LMAX; L++)
         for (uint32_t d = 0; d < 2; d++) {
             const uint32_t N = 1u << L, delta = d ? N : 0;
             uint32_t* img = &t.col_img[col_img_offset(L, d)];
@@ -164,12 +164,14 @@ void build(HostTables& t) {
         };
         auto mod = [](int64_t v) { return (uint32_t)(((v % 65535) + 65535) % 65535); };
         fwht(w.data(), GF_ORDER);
-        t.col_v.assign(2048 + 1024, 0);
-        for (uint32_t n : {2048u, 1024u}) {
+        t.col_v.assign(COL_V_DWORDS, 0);
+        for (uint32_t n = 2u << COL_LMIN; n <= (2u << COL_LMAX); n <<= 1) {
             std::vector<int64_t> v(n);
             for (uint32_t i = 0; i < n; i++) v[i] = mod(w[i]);
             fwht(v.data(), n);
-            const int64_t inv = n == 2048 ? 32 : 64;  // 2^-11 / 2^-10 mod 65535 (2^16 = 1)
+            uint32_t lg = 0;
+            while ((1u << lg) < n) lg++;
+            const int64_t inv = (int64_t)1 << (16 - lg);  // n^-1 = 2^(16 - log2 n) mod 65535 (2^16 = 1)
             for (uint32_t k = 0; k < n; k++) t.col_v[col_v_offset(n) + k] = mod(mod(v[k]) * inv);
         }
     }

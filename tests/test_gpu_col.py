@@ -62,7 +62,9 @@ def dev_decode(eng, original, recovery, orig_mask, rec_mask):
 # (k, m): chunk = 512 / 1024 rows on the high-rate side, and low-rate cases
 # whose one recovery chunk is 512 / 1024 rows
 CASES = [(1, 257), (100, 300), (257, 512), (512, 512), (300, 1000), (1000, 1000), (1024, 1024), (511, 513),
-         (700, 600), (1000, 520), (1024, 600), (600, 1024)]
+         (700, 600), (1000, 520), (1024, 600), (600, 1024),
+         # 64 / 128 / 256-row transforms (one wave or less per workgroup)
+         (50, 60), (100, 100), (30, 100), (200, 256), (256, 129), (100, 40), (64, 33), (1, 64)]
 
 
 @pytest.mark.parametrize("k,m", CASES)
@@ -99,7 +101,7 @@ def test_col_matches_pass_codec(eng, k, m, no_column):
 
 
 @pytest.mark.parametrize("k,m", [(1000, 1000), (512, 512), (257, 300), (100, 1000), (1024, 1024), (600, 1024),
-                                 (1000, 520)])
+                                 (1000, 520), (100, 100), (60, 64), (200, 256), (33, 64), (128, 200)])
 @pytest.mark.parametrize("lost_rec", [0, 5])
 def test_col_half_decode(eng, k, m, lost_rec):
     """Every original lost, recovery shards given (some of them lost too):
@@ -118,7 +120,7 @@ def test_col_half_decode(eng, k, m, lost_rec):
 
 
 @pytest.mark.parametrize("rate", ["high", "low"])
-@pytest.mark.parametrize("k,m", [(1000, 1000), (512, 300), (300, 512)])
+@pytest.mark.parametrize("k,m", [(1000, 1000), (512, 300), (300, 512), (100, 100), (200, 60)])
 def test_col_rate_api_in_place(eng, rate, k, m):
     """The Rate API's work buffer: originals, recovery and restored rows
     share one array (in == out for the column encode)."""
@@ -146,7 +148,7 @@ def test_col_rate_api_in_place(eng, rate, k, m):
 
 
 @pytest.mark.parametrize("k,m,n,sb", [(1000, 1000, 5, 128), (512, 512, 3, 128), (300, 1000, 4, 128),
-                                      (1000, 1000, 6, 1024)])
+                                      (1000, 1000, 6, 1024), (100, 100, 7, 192)])
 def test_col_batched_stripes(eng, k, m, n, sb, force_column):
     pad = 64
     so, sr = k * sb + pad, m * sb + pad
@@ -197,11 +199,12 @@ def test_col_host_multi(eng):
     assert np.array_equal(rec, O.encode(k, m, original))
 
 
-def test_col_decode_check_counts(eng):
+@pytest.mark.parametrize("k,m", [(900, 1000), (100, 120)])
+def test_col_decode_check_counts(eng, k, m):
     """The column decoder evaluates the polynomial itself (no eval kernel) and
     writes the per-chunk received counts rs16_decode_check reads: a caller
     whose counts disagree with its flags gets InvalidArgument."""
-    k, m, sb = 900, 1000, 64
+    sb = 64
     original = generate_original(k, sb, 5)
     recovery = O.encode(k, m, original)
     d_orig = DeviceArray.from_numpy(eng, np.zeros_like(original))
