@@ -290,12 +290,12 @@ __device__ __forceinline__ uint32_t mod65535(int v) { return fold65535((uint32_t
 // (x[j] in thread t): register layers (bits of j), lane layers (shuffles),
 // wave layers through the LDS scratch `sx` (n ints).  Ends with a barrier
 // (sx free again).
-template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* sx) {
+template <int NT, int PTS> __device__ __forceinline__ void fwht_points(int (&x)[PTS], int* sx) {
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
-    for (int d = 1; d < 8; d <<= 1)
+    for (int d = 1; d < PTS; d <<= 1)
 #pragma unroll
-        for (int j = 0; j < 8; j++)
+        for (int j = 0; j < PTS; j++)
             if (!(j & d)) {
                 const int u = x[j], v = x[j + d];
                 x[j] = u + v;
@@ -303,7 +303,7 @@ template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* 
             }
 #define RS16_LANE(D)                                              \
     if constexpr ((D) < NT) {                                     \
-        _Pragma("unroll") for (int j = 0; j < 8; j++) {           \
+        _Pragma("unroll") for (int j = 0; j < PTS; j++) {         \
             const int p = xshfl<(D)>(x[j]);                       \
             x[j] = (lane & (D)) ? p - x[j] : x[j] + p;            \
         }                                                         \
@@ -315,7 +315,7 @@ template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* 
 #pragma unroll
     for (int lb = 4; lb <= 5 && (1 << lb) < NT; lb++)
 #pragma unroll
-        for (int j = 0; j < 8; j += 2) {
+        for (int j = 0; j < PTS; j += 2) {
             auto sw = [&]() {
                 const auto r = lb == 4 ? __builtin_amdgcn_permlane16_swap((uint32_t)x[j], (uint32_t)x[j + 1], false, false)
                                        : __builtin_amdgcn_permlane32_swap((uint32_t)x[j], (uint32_t)x[j + 1], false, false);
@@ -331,10 +331,10 @@ template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* 
     constexpr int NW = NT / 64;
     if constexpr (NW > 1) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) sx[t + NT * j] = x[j];
+        for (int j = 0; j < PTS; j++) sx[t + NT * j] = x[j];
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < PTS; j++) {
             int acc = 0;
 #pragma unroll
             for (int v = 0; v < NW; v++) {
@@ -347,31 +347,33 @@ template <int NT> __device__ __forceinline__ void fwht_points(int (&x)[8], int* 
     }
 }
 
-// The erasure logs of work rows [0, 2N) into elds, and the received counts
-// per 64-row chunk (rcount, workgroup 0) for rs16_decode_check.  Segment A =
-// recovery rows [0, in_rows) (flags), [in_rows, N) padding (erased), segment
-// B = originals [N, N + o_rows) (flags_o) (rate_high.rs:183-197).
-template <int L> __device__ __forceinline__ void col_eval(const ColArgs& a, uint32_t* elds) {
+// The erasure logs of work rows [0, NT PTS) into elds, and the received
+// counts per 64-row chunk (rcount, workgroup 0) for rs16_decode_check.
+// Segment A = recovery rows [0, in_rows) (flags), [in_rows, chunk) padding
+// (erased), segment B = originals [chunk, chunk + o_rows) (flags_o), zero
+// above (rate_high.rs:183-197).  PTS = 8: the half decode's 2N work rows;
+// PTS = 4: the general decode's N.
+template <int L, int PTS> __device__ __forceinline__ void col_eval(const ColArgs& a, uint32_t* elds) {
     constexpr int N = 1 << L, NT = N / 4;
     const uint32_t t = threadIdx.x, lane = t & 63;
-    uint8_t f[8];
-    uint32_t vt[8];
+    uint8_t f[PTS];
+    uint32_t vt[PTS];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < PTS; j++) {
         const uint32_t p = t + NT * j;
-        const bool in_a = p < a.in_rows, in_b = p >= N && p - N < a.o_rows;
-        const uint8_t* fp = in_a && a.flags ? a.flags + p : (in_b && a.flags_o ? a.flags_o + (p - N) : a.zero);
+        const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
+        const uint8_t* fp = in_a && a.flags ? a.flags + p : (in_b && a.flags_o ? a.flags_o + (p - a.chunk) : a.zero);
         f[j] = *(const __attribute__((address_space(1))) uint8_t*)fp;
         vt[j] = a.vtab[p];
     }
-    int x[8];
+    int x[PTS];
     uint32_t ca = 0, cb = 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < PTS; j++) {
         const uint32_t p = t + NT * j;
-        const bool in_a = p < a.in_rows, in_b = p >= N && p - N < a.o_rows;
+        const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
         const bool rcv = in_a ? (!a.flags || f[j]) : (in_b && (!a.flags_o || f[j]));
-        x[j] = (in_a || in_b) ? !rcv : (p < N);
+        x[j] = (in_a || in_b) ? !rcv : (p < a.chunk);
         if (blockIdx.x == 0 && a.rcount) {
             // (below 64 threads a 64-row chunk spans 64 / NT values of j)
             constexpr int PER = NT >= 64 ? 1 : 64 / NT;
@@ -387,17 +389,52 @@ template <int L> __device__ __forceinline__ void col_eval(const ColArgs& a, uint
         }
     }
     int* sx = (int*)elds;
-    fwht_points<NT>(x, sx);
+    fwht_points<NT, PTS>(x, sx);
 #pragma unroll
-    for (int j = 0; j < 8; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
-    fwht_points<NT>(x, sx);
+    for (int j = 0; j < PTS; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
+    fwht_points<NT, PTS>(x, sx);
 #pragma unroll
-    for (int j = 0; j < 8; j++) elds[t + NT * j] = mod65535(x[j]);
+    for (int j = 0; j < PTS; j++) elds[t + NT * j] = mod65535(x[j]);
+}
+
+// The formal derivative (Engine::formal_derivative, src/engine.rs:233-238) of
+// the whole column, in the closed form out[j] = d[j] ^ XOR{ d[j | 2^b] : bit b
+// of j is 0 }, between the general decoder's IFFT and FFT:
+// register bits from registers, every other bit from an LDS image of d.
+template <int L, int B0, int B1>
+__device__ __forceinline__ void col_fd(uint32_t (&XL)[4], uint32_t (&XH)[4], uint32_t t, uint8_t* smem) {
+    uint2* img = (uint2*)(smem + ColSmem<L>::IMG);
+    __syncthreads();  // (every wave is past its IFFT tables and earlier image reads)
+#pragma unroll
+    for (int m = 0; m < 4; m++) img[swz(brow<B0, B1>(t, m))] = make_uint2(XL[m], XH[m]);
+    __syncthreads();
+    uint32_t AL[4], AH[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const uint32_t j = brow<B0, B1>(t, m);
+        uint32_t al = XL[m], ah = XH[m];
+        if (!(m & 1)) al ^= XL[m | 1], ah ^= XH[m | 1];
+        if (!(m & 2)) al ^= XL[m | 2], ah ^= XH[m | 2];
+#pragma unroll
+        for (int b = 0; b < L; b++) {
+            if (b == B0 || b == B1) continue;
+            const uint2 v = img[swz(j | (1u << b))];
+            const bool take = !((j >> b) & 1u);
+            al ^= take ? v.x : 0u;
+            ah ^= take ? v.y : 0u;
+        }
+        AL[m] = al;
+        AH[m] = ah;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++) XL[m] = AL[m], XH[m] = AH[m];
+    __syncthreads();  // (the image is free again)
 }
 
 template <int L, int MODE>
 __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
-    constexpr bool DEC = MODE != COL_ENC, EVAL = MODE == COL_DEC_EVAL;
+    constexpr bool DEC = MODE != COL_ENC, GEN = MODE == COL_DEC_GEN;
+    constexpr bool EVAL = MODE == COL_DEC_EVAL || GEN;  // the polynomial in the kernel
     constexpr int N = 1 << L, NT = N / 4;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t t = threadIdx.x;
@@ -427,23 +464,32 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         const uint32_t r = 4 * t + m;
         // (a row that is not read comes from the zero page, RS16_ZERO_BYTES;
         // the decoder zeroes rows that were not received with its multiply)
-        const uint32_t* p = (const uint32_t*)(r < a.in_rows ? in + (size_t)r * a.S_in : a.zero + (offL & 0x7FFFu));
+        const uint8_t* src = a.zero + (offL & 0x7FFFu);
+        if (r < a.in_rows) src = in + (size_t)r * a.S_in;
+        // (the general decoder also gathers the received originals, rows [chunk, chunk + o_rows))
+        if (GEN && r >= a.chunk && r - a.chunk < a.o_rows) src = a.in_b + st * a.bs_in_b + offL + (size_t)(r - a.chunk) * a.S_in;
+        const uint32_t* p = (const uint32_t*)src;
         XL[m] = p[0];
         XH[m] = p[8];
     }
     dma_tables();
     uint32_t gt[DEC ? 4 : 1][20];
     uint32_t ev[4] = {0, 0, 0, 0};
+    bool lost[4] = {false, false, false, false};  // (GEN: the row is a lost original)
     if constexpr (DEC) {
         bool rcv[4];
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             const uint32_t r = 4 * t + m;
             rcv[m] = r < a.in_rows && (!a.flags || a.flags[r] != 0);
+            if (GEN && r >= a.chunk && r - a.chunk < a.o_rows) {
+                rcv[m] = !a.flags_o || a.flags_o[r - a.chunk] != 0;
+                lost[m] = !rcv[m];
+            }
         }
         uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
         if constexpr (EVAL) {
-            col_eval<L>(a, elds);
+            col_eval<L, GEN ? 4 : 8>(a, elds);
             __syncthreads();
         } else if constexpr (L >= 9) {
             // eval_poly's output before its last 256-point FWHT (a.elog = the
@@ -507,6 +553,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     if constexpr (L == 6) {
         // the FFT's first block keeps the row bits (4, 5)
         cstamp(a, 5);
+        if constexpr (GEN) col_fd<L, 4, 5>(XL, XH, t, smem);
         load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
         cstamp(a, 6);
     } else if constexpr (L == 7) {
@@ -515,6 +562,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         swap_bit<1, 4>(XH);
         compute<false, false, true>(XL, XH, tb);
         cstamp(a, 5);
+        if constexpr (GEN) col_fd<L, 4, 6>(XL, XH, t, smem);
         load_tabs<L, true, 4, 6, false, true>(tb, t, smem);
         compute<true, false, true>(XL, XH, tb);
         load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
@@ -527,6 +575,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         compute<false, true, true>(XL, XH, tb);
         if constexpr (L == 8) {
             cstamp(a, 5);
+            if constexpr (GEN) col_fd<L, 6, 7>(XL, XH, t, smem);
             load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
         } else if constexpr (L == 10) {
             load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
@@ -535,6 +584,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             exchange<6, 7, 8, 9>(XL, XH, t, smem);
             compute<false, true, true>(XL, XH, ta);
             cstamp(a, 5);
+            if constexpr (GEN) col_fd<L, 8, 9>(XL, XH, t, smem);
             // the FFT's first block keeps the row bits: no exchange
             load_tabs<L, true, 8, 9, true, true>(tb, t, smem);
             compute<true, true, true>(XL, XH, tb);
@@ -548,6 +598,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             exchange<6, 7, 7, 8>(XL, XH, t, smem);
             compute<false, false, true>(XL, XH, ta);
             cstamp(a, 5);
+            if constexpr (GEN) col_fd<L, 7, 8>(XL, XH, t, smem);
             load_tabs<L, true, 7, 8, false, true>(tb, t, smem);
             compute<true, false, true>(XL, XH, tb);
             load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
@@ -594,8 +645,9 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             vl = zl;
             vh = zh;
         }
-        if (r < a.out_rows) {
-            uint32_t* p = (uint32_t*)(out + (size_t)r * a.S_out);
+        const bool st_ok = GEN ? lost[m] : r < a.out_rows;
+        if (st_ok) {
+            uint32_t* p = (uint32_t*)(out + (size_t)(GEN ? r - a.chunk : r) * a.S_out);
             __builtin_nontemporal_store(vl, p);
             __builtin_nontemporal_store(vh, p + 8);
         }
@@ -612,12 +664,13 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
 int col_rows_ok(uint32_t L) { return L >= COL_LMIN && L <= COL_LMAX; }
 
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
-    if (!col_rows_ok(L) || mode < COL_ENC || mode > COL_DEC_EVAL) return hipErrorInvalidValue;
+    if (!col_rows_ok(L) || mode < COL_ENC || mode > COL_DEC_GEN) return hipErrorInvalidValue;
     if (a.qrow == 0 || a.nstripes == 0 || a.out_rows == 0) return hipSuccess;
     typedef void (*ColFn)(ColArgs);
-#define RS16_COL_ROW(L) \
-    {col_kernel<L, COL_ENC>, L >= 9 ? col_kernel<L, COL_DEC_EWORK> : nullptr, col_kernel<L, COL_DEC_EVAL>}
-    static const ColFn fns[5][3] = {RS16_COL_ROW(6), RS16_COL_ROW(7), RS16_COL_ROW(8), RS16_COL_ROW(9),
+#define RS16_COL_ROW(L)                                                                                   \
+    {col_kernel<L, COL_ENC>, L >= 9 ? col_kernel<L, COL_DEC_EWORK> : nullptr, col_kernel<L, COL_DEC_EVAL>, \
+     col_kernel<L, COL_DEC_GEN>}
+    static const ColFn fns[5][4] = {RS16_COL_ROW(6), RS16_COL_ROW(7), RS16_COL_ROW(8), RS16_COL_ROW(9),
                                     RS16_COL_ROW(10)};
 #undef RS16_COL_ROW
     static const int lds[5] = {ColSmem<6>::BYTES, ColSmem<7>::BYTES, ColSmem<8>::BYTES, ColSmem<9>::BYTES,

@@ -265,7 +265,8 @@ int rs16_engine::col(const ColArgs& args, int L, int mode, hipStream_t s, rs16_e
         return hip_fail(err, hipErrorInvalidValue);  // (unreachable: every caller passes 0 or 2^L)
     a.img_ifft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_ifft ? 1 : 0));
     a.img_fft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_fft ? 1 : 0));
-    if (mode == COL_DEC_EVAL) a.vtab = d_col_v + col_v_offset(2u << L);
+    if (mode == COL_DEC_EVAL) a.vtab = d_col_v + col_v_offset(2u << L);  // (2^(L+1) work rows)
+    if (mode == COL_DEC_GEN) a.vtab = d_col_v + col_v_offset(1u << L);   // (2^L work rows)
     hipEvent_t ev;
     const int prof = dec ? PROF_COL_DEC : PROF_COL_ENC;
     if (int rc = prof_begin(s, &ev, err)) return rc;
@@ -438,7 +439,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // High-rate half decodes of 2^9 / 2^10-row halves through the column
     // codec: it evaluates the polynomial itself (an n-point XOR convolution,
     // rs16_col.hip) and writes rcount; no kernel here.
-    eval_in_col = S && g.high && half_decode(g) && col_ok(ilog2(g.n) - 1, S, nstripes);
+    eval_in_col = S && g.high && col_ok(ilog2(g.n) - (half_decode(g) ? 1 : 0), S, nstripes);
     if (eval_in_col) return RS16_OK;
     es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
     hipEvent_t ev;
@@ -544,6 +545,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
             c.out_rows = orig;
             c.base_in = c.skew_ifft = src;
             c.base_out = c.skew_fft = dst;
+            c.chunk = g.chunk;
             if (col_eval) {
                 // eval_poly in the kernel (decode_eval launched nothing)
                 c.flags_o = flags_b;
@@ -566,6 +568,28 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         a.out = nullptr;
         RS16_PASS(DEC_HALF_LAST, lo, a, batch((orig + (1u << lo) - 1) >> lo, zs, 0, 0), s);
         return RS16_OK;
+    }
+    if (eval_in_col && g.high) {
+        // up to 2^10 work rows: the whole general decode in one launch,
+        // polynomial and formal derivative in the kernel (rs16_col.hip)
+        ColArgs c = col_args();
+        c.in = seg_a;
+        c.flags = flags_a;
+        c.in_rows = g.a_count;
+        c.in_b = seg_b;
+        c.bs_in_b = bs_b;
+        c.flags_o = flags_b;
+        c.o_rows = g.b_count;
+        c.chunk = g.chunk;
+        c.out = rest;
+        c.S_in = c.S_out = S_user;
+        c.qrow = (uint32_t)(S / 8);
+        c.nstripes = ns;
+        c.bs_in = bs_a;
+        c.bs_out = bs_rest;
+        c.out_rows = g.b_count;
+        c.rcount = (uint32_t*)ws_rcount.p;
+        return col(c, L, COL_DEC_GEN, s, err);
     }
     if (L <= 8) {
         RS16_PASS(DEC_SINGLE, L, a, batch(1, 0, 0, 0), s);

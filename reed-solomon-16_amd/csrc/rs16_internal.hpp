@@ -33,8 +33,8 @@ constexpr size_t col_img_offset(uint32_t L, uint32_t d) {
     return off + (size_t)d * ((1u << L) - 1) * 20;
 }
 constexpr size_t COL_IMG_DWORDS = col_img_offset(COL_LMAX + 1, 0);
-// n = 2^(COL_LMIN+1) .. 2^(COL_LMAX+1): tables of n entries at n - 2^(COL_LMIN+1)
-constexpr size_t col_v_offset(uint32_t n) { return n - (2u << COL_LMIN); }
+// n = 2^COL_LMIN .. 2^(COL_LMAX+1): tables of n entries at n - 2^COL_LMIN
+constexpr size_t col_v_offset(uint32_t n) { return n - (1u << COL_LMIN); }
 constexpr size_t COL_V_DWORDS = col_v_offset(4u << COL_LMAX);
 const HostTables& host_tables();
 
@@ -178,6 +178,10 @@ struct ColArgs {
     uint32_t o_rows;
     const uint32_t* vtab;
     uint32_t* rcount;
+    uint32_t chunk;             // decoder: first row of segment B (the originals)
+    // COL_DEC_GEN: the received originals (segment B rows, stride S_in, stripe stride bs_in_b)
+    const uint8_t* in_b;
+    uint64_t bs_in_b;
     const uint8_t* in;
     const uint8_t* flags;
     uint8_t* out;
@@ -195,7 +199,9 @@ struct ColArgs {
     uint64_t* stamps;           // RS16_STAMPS builds: phase timeline (rs16_engine_set_stamps)
 };
 int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec covers
-enum ColMode : int { COL_ENC = 0, COL_DEC_EWORK, COL_DEC_EVAL };
+// COL_DEC_GEN: the general high-rate decode of a 2^L-row work buffer (any
+// loss pattern; formal derivative in the kernel), polynomial in the kernel
+enum ColMode : int { COL_ENC = 0, COL_DEC_EWORK, COL_DEC_EVAL, COL_DEC_GEN };
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s);
 
 // Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):

@@ -165,7 +165,7 @@ void build(HostTables& t) {
         auto mod = [](int64_t v) { return (uint32_t)(((v % 65535) + 65535) % 65535); };
         fwht(w.data(), GF_ORDER);
         t.col_v.assign(COL_V_DWORDS, 0);
-        for (uint32_t n = 2u << COL_LMIN; n <= (2u << COL_LMAX); n <<= 1) {
+        for (uint32_t n = 1u << COL_LMIN; n <= (2u << COL_LMAX); n <<= 1) {
             std::vector<int64_t> v(n);
             for (uint32_t i = 0; i < n; i++) v[i] = mod(w[i]);
             fwht(v.data(), n);

@@ -94,13 +94,13 @@ def conv_eval(e, n):
     H(LogWalsh . H(e)) are the XOR convolution e (*) W, W = H(LogWalsh):
     H_n(H_n(e) . V), V = n^-1 H_n(W[0, n)) mod 65535, n^-1 = 2^(16 - log2 n)."""
     w = _fwht_int(O.table("log_walsh")) % 65535
-    inv = {2048: 32, 1024: 64}[n]
+    inv = 1 << (16 - (n.bit_length() - 1))  # n^-1 = 2^(16 - log2 n) mod 65535
     v = (_fwht_int(w[:n]) % 65535) * inv % 65535
     x = _fwht_int(e[:n]) % 65535
     return _fwht_int((x * v) % 65535) % 65535
 
 
-@pytest.mark.parametrize("n", [1024, 2048])
+@pytest.mark.parametrize("n", [64, 256, 1024, 2048])
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_conv_eval_matches_oracle(n, seed):
     rng = np.random.default_rng(seed * 7 + n)

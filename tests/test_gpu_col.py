@@ -216,3 +216,44 @@ def test_col_decode_check_counts(eng, k, m):
     with pytest.raises(rs16.Error) as e:
         rs16.decode_device(k, m, sb, d_orig.ptr, d_of.ptr, d_rec.ptr, d_rf.ptr, 0, m - 1, engine=eng, check=True)
     assert e.value.kind == "InvalidArgument"
+
+
+@pytest.mark.parametrize("k,m", [(100, 100), (300, 300), (200, 256), (50, 60), (512, 512), (33, 64), (700, 300)])
+@pytest.mark.parametrize("pattern", ["1pct", "random", "mixed"])
+def test_col_general_decode(eng, k, m, pattern):
+    """The general decode (any loss pattern) of up to 1024 work rows in one
+    launch: polynomial, gather of both segments, IFFT, formal derivative, FFT,
+    reveal (rate_high.rs:168-247); every lost original restored bit for bit,
+    received originals untouched."""
+    sb = 64
+    original = generate_original(k, sb, 3 * k + m)
+    recovery = O.encode(k, m, original)
+    rng = np.random.default_rng(k + 5 * m)
+    om, rm = np.ones(k, bool), np.zeros(m, bool)
+    if pattern == "1pct":  # benches/benchmarks.rs:81-105
+        loss = max(1, min(k, m) // 100)
+        om[k - loss:] = False
+        rm[:loss] = True
+    else:
+        loss = int(rng.integers(1, min(k, m) + 1)) if pattern == "random" else min(k, m) // 2
+        om[rng.choice(k, loss, replace=False)] = False
+        rm[rng.choice(m, min(m, loss + (3 if m > loss + 3 else 0)), replace=False)] = True
+    if rm.sum() + om.sum() < k:
+        pytest.skip("not enough shards")
+    assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+
+
+def test_col_general_decode_matches_pass_codec(eng, no_column):
+    k, m, sb = 300, 300, 128
+    original = generate_original(k, sb, 17)
+    recovery = O.encode(k, m, original)
+    om, rm = np.ones(k, bool), np.zeros(m, bool)
+    om[::7] = False
+    rm[:60] = True
+    want = dev_decode(eng, original, recovery, om, rm)
+    old = rs16.set_diagnostics(0)
+    try:
+        got = dev_decode(eng, original, recovery, om, rm)
+    finally:
+        rs16.set_diagnostics(old)
+    assert np.array_equal(got, want) and np.array_equal(got, original)
