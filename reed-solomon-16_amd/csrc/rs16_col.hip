@@ -88,6 +88,21 @@ template <int L> struct ColSmem {
     static_assert(L >= (int)COL_LMIN && L <= (int)COL_LMAX, "the column codec covers 2^6 .. 2^10 rows");
 };
 
+// The general decoder's 2^11-row transform (COL_DEC_GEN only): the tables
+// of layers 0 and 1 are each used by one thread once, so they are read from
+// the image in HBM / L2 at their block; LDS holds layers 2..10 of both
+// directions, the row image and the erasure logs side by side.
+template <> struct ColSmem<11> {
+    static constexpr int N = 2048;
+    static constexpr int G0 = N - N / 4;  // first group of layer 2
+    static constexpr int A = 0;
+    static constexpr int B = A + (N - 1 - G0) * 80;
+    static constexpr int IMG = B + (N - 1 - G0) * 80;
+    static constexpr int ELOG = IMG + N * 8;
+    static constexpr int C = -1;  // (unused)
+    static constexpr int BYTES = ELOG + N * 4;
+};
+
 __device__ __forceinline__ void lds_table(uint32_t (&t)[20], const uint8_t* smem, uint32_t off) {
     const u32x4* p = (const u32x4*)(smem + off);
 #pragma unroll
@@ -115,6 +130,7 @@ __device__ __forceinline__ void glb_table(uint32_t (&t)[20], const uint32_t* tab
 template <int L, bool FFT> __device__ __forceinline__ uint32_t tab_off(int kb, uint32_t r) {
     constexpr int N = 1 << L;
     const uint32_t t = (uint32_t)(N - (N >> kb)) + (r >> (kb + 1));
+    if constexpr (L == 11) return (FFT ? ColSmem<11>::B : ColSmem<11>::A) + (t - ColSmem<11>::G0) * 80u;
     if (!FFT) return ColSmem<L>::A + t * 80u;
     if (kb == 0) return ColSmem<L>::C + t * 80u;
     return ColSmem<L>::B + (t - N / 2) * 80u;
@@ -185,6 +201,26 @@ __device__ __forceinline__ void load_tabs(BlockTabs& w, uint32_t t, const uint8_
     }
     if (D1) lds_table(w.w1, smem, tab_off<L, FFT>(B1, r0));
 }
+// The (0, 1) block's tables at L = 11, from the image (table g at g x 80 bytes).
+__device__ __forceinline__ void img_table(uint32_t (&t)[20], const uint8_t* img, uint32_t g) {
+    const u32x4* p = (const u32x4*)(img + (size_t)g * 80);
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const u32x4 v = p[i];
+        t[4 * i] = v.x;
+        t[4 * i + 1] = v.y;
+        t[4 * i + 2] = v.z;
+        t[4 * i + 3] = v.w;
+    }
+}
+__device__ __forceinline__ void load_tabs01_img(BlockTabs& w, uint32_t t, const uint8_t* img) {
+    constexpr uint32_t N = 2048;
+    const uint32_t r0 = brow<0, 1>(t, 0), r2 = brow<0, 1>(t, 2);
+    img_table(w.w0, img, r0 >> 1);
+    img_table(w.w2, img, r2 >> 1);
+    img_table(w.w1, img, N / 2 + (r0 >> 2));
+}
+
 template <bool FFT, bool D0, bool D1>
 __device__ __forceinline__ void compute(uint32_t (&XL)[4], uint32_t (&XH)[4], const BlockTabs& w) {
     auto lay0 = [&]() {
@@ -455,8 +491,14 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     // load while one is in flight: the decoder's polynomial starts once the
     // tables are in)
     auto dma_tables = [&]() {
-        dma_copy<NT>(a.img_ifft, smem + ColSmem<L>::A, (N - 1) * 80);
-        dma_copy<NT>(a.img_fft + (N / 2) * 80, smem + ColSmem<L>::B, (N / 2 - 1) * 80);
+        if constexpr (L == 11) {
+            constexpr int G0 = ColSmem<11>::G0;
+            dma_copy<NT>(a.img_ifft + G0 * 80, smem + ColSmem<L>::A, (N - 1 - G0) * 80);
+            dma_copy<NT>(a.img_fft + G0 * 80, smem + ColSmem<L>::B, (N - 1 - G0) * 80);
+        } else {
+            dma_copy<NT>(a.img_ifft, smem + ColSmem<L>::A, (N - 1) * 80);
+            dma_copy<NT>(a.img_fft + (N / 2) * 80, smem + ColSmem<L>::B, (N / 2 - 1) * 80);
+        }
     };
     uint32_t XL[4], XH[4];
 #pragma unroll
@@ -532,7 +574,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     __syncthreads();
     cstamp(a, 2);
     // the FFT's layer-0 tables into C (the decoder's logs there are read)
-    dma_copy<NT>(a.img_fft, smem + ColSmem<L>::C, (N / 2) * 80);
+    if constexpr (L <= 10) dma_copy<NT>(a.img_fft, smem + ColSmem<L>::C, (N / 2) * 80);
 
     // ---- IFFT (layers 0 .. L-1) then FFT (L-1 .. 0) in radix-4 blocks; the
     // next block's tables are read before each exchange.  Row bits 0-5 are
@@ -540,6 +582,55 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     // are wave bits (two LDS exchanges); L = 7 ends with a one-layer block on
     // bits (4, 6).
     BlockTabs ta, tb;
+  if constexpr (L == 11) {
+    // the general decoder over 2^11 work rows (8 waves; row bits 6-10 of
+    // some blocks are wave bits: four LDS exchanges, the last IFFT / first
+    // FFT layer as a one-layer block on bits (8, 10))
+    static_assert(GEN, "2^11 rows: the general decoder only");
+    load_tabs01_img(ta, t, a.img_ifft);
+    compute<false, true, true>(XL, XH, ta);
+    cstamp(a, 3);
+    load_tabs<L, false, 2, 3, true, true>(tb, t, smem);
+    wave_exchange<0, 1>(XL, XH);
+    compute<false, true, true>(XL, XH, tb);
+    load_tabs<L, false, 4, 5, true, true>(ta, t, smem);
+    wave_exchange<2, 3>(XL, XH);
+    compute<false, true, true>(XL, XH, ta);
+    cstamp(a, 4);
+    load_tabs<L, false, 6, 7, true, true>(tb, t, smem);
+    wave_exchange<4, 5>(XL, XH);
+    compute<false, true, true>(XL, XH, tb);
+    load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
+    exchange<6, 7, 8, 9>(XL, XH, t, smem);
+    compute<false, true, true>(XL, XH, ta);
+    load_tabs<L, false, 8, 10, false, true>(tb, t, smem);
+    __syncthreads();  // (every wave has read its rows of the image)
+    exchange<8, 9, 8, 10>(XL, XH, t, smem);
+    compute<false, false, true>(XL, XH, tb);
+    cstamp(a, 5);
+    col_fd<L, 8, 10>(XL, XH, t, smem);
+    load_tabs<L, true, 8, 10, false, true>(tb, t, smem);
+    compute<true, false, true>(XL, XH, tb);
+    load_tabs<L, true, 8, 9, true, true>(ta, t, smem);
+    __syncthreads();
+    exchange<8, 10, 8, 9>(XL, XH, t, smem);
+    compute<true, true, true>(XL, XH, ta);
+    cstamp(a, 6);
+    load_tabs<L, true, 6, 7, true, true>(tb, t, smem);
+    __syncthreads();
+    exchange<8, 9, 6, 7>(XL, XH, t, smem);
+    compute<true, true, true>(XL, XH, tb);
+    load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
+    wave_exchange<4, 5>(XL, XH);
+    compute<true, true, true>(XL, XH, ta);
+    cstamp(a, 7);
+    load_tabs<L, true, 2, 3, true, true>(tb, t, smem);
+    wave_exchange<2, 3>(XL, XH);
+    compute<true, true, true>(XL, XH, tb);
+    load_tabs01_img(tb, t, a.img_fft);
+    wave_exchange<0, 1>(XL, XH);
+    cstamp(a, 8);
+  } else {
     load_tabs<L, false, 0, 1, true, true>(ta, t, smem);
     compute<false, true, true>(XL, XH, ta);
     cstamp(a, 3);
@@ -624,6 +715,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     load_tabs<L, true, 0, 1, true, true>(tb, t, smem);
     wave_exchange<0, 1>(XL, XH);
     cstamp(a, 8);
+  }
     uint32_t rt[DEC ? 4 : 1][20];
     if constexpr (DEC) {
         // reveal multipliers (requested here so the tables are in flight
@@ -664,17 +756,18 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
 int col_rows_ok(uint32_t L) { return L >= COL_LMIN && L <= COL_LMAX; }
 
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
-    if (!col_rows_ok(L) || mode < COL_ENC || mode > COL_DEC_GEN) return hipErrorInvalidValue;
+    if (L < COL_LMIN || L > COL_LGEN || mode < COL_ENC || mode > COL_DEC_GEN) return hipErrorInvalidValue;
+    if (L == COL_LGEN && mode != COL_DEC_GEN) return hipErrorInvalidValue;
     if (a.qrow == 0 || a.nstripes == 0 || a.out_rows == 0) return hipSuccess;
     typedef void (*ColFn)(ColArgs);
 #define RS16_COL_ROW(L)                                                                                   \
     {col_kernel<L, COL_ENC>, L >= 9 ? col_kernel<L, COL_DEC_EWORK> : nullptr, col_kernel<L, COL_DEC_EVAL>, \
      col_kernel<L, COL_DEC_GEN>}
-    static const ColFn fns[5][4] = {RS16_COL_ROW(6), RS16_COL_ROW(7), RS16_COL_ROW(8), RS16_COL_ROW(9),
-                                    RS16_COL_ROW(10)};
+    static const ColFn fns[6][4] = {RS16_COL_ROW(6),  RS16_COL_ROW(7), RS16_COL_ROW(8), RS16_COL_ROW(9),
+                                    RS16_COL_ROW(10), {nullptr, nullptr, nullptr, col_kernel<11, COL_DEC_GEN>}};
 #undef RS16_COL_ROW
-    static const int lds[5] = {ColSmem<6>::BYTES, ColSmem<7>::BYTES, ColSmem<8>::BYTES, ColSmem<9>::BYTES,
-                               ColSmem<10>::BYTES};
+    static const int lds[6] = {ColSmem<6>::BYTES, ColSmem<7>::BYTES,  ColSmem<8>::BYTES,
+                               ColSmem<9>::BYTES, ColSmem<10>::BYTES, ColSmem<11>::BYTES};
     const ColFn fn = fns[L - COL_LMIN][mode];
     if (!fn) return hipErrorInvalidValue;  // (the ework decoder needs 4 waves: L >= 9)
     const int bytes = lds[L - COL_LMIN];

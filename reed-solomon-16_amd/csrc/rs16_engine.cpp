@@ -215,8 +215,9 @@ int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStr
     return prof_end(prof, s, ev, err);
 }
 
-bool rs16_engine::col_ok(int L, size_t S, size_t nstripes) const {
-    if (!col_rows_ok((uint32_t)L) || (g_diag & DIAG_NO_COLUMN)) return false;
+bool rs16_engine::col_ok(int L, size_t S, size_t nstripes, bool gen) const {
+    const bool rows = col_rows_ok((uint32_t)L) || (gen && L == (int)COL_LGEN);
+    if (!rows || (g_diag & DIAG_NO_COLUMN)) return false;
     return (S / 8) * nstripes <= col_max_quads || (g_diag & DIAG_FORCE_COLUMN);
 }
 
@@ -439,7 +440,8 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // High-rate half decodes of 2^9 / 2^10-row halves through the column
     // codec: it evaluates the polynomial itself (an n-point XOR convolution,
     // rs16_col.hip) and writes rcount; no kernel here.
-    eval_in_col = S && g.high && col_ok(ilog2(g.n) - (half_decode(g) ? 1 : 0), S, nstripes);
+    eval_in_col = S && g.high &&
+                  (half_decode(g) ? col_ok(ilog2(g.n) - 1, S, nstripes) : col_ok(ilog2(g.n), S, nstripes, true));
     if (eval_in_col) return RS16_OK;
     es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
     hipEvent_t ev;

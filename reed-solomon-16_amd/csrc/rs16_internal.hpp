@@ -32,7 +32,9 @@ constexpr size_t col_img_offset(uint32_t L, uint32_t d) {
     for (uint32_t l = COL_LMIN; l < L; l++) off += 2 * ((1u << l) - 1) * 20;
     return off + (size_t)d * ((1u << L) - 1) * 20;
 }
-constexpr size_t COL_IMG_DWORDS = col_img_offset(COL_LMAX + 1, 0);
+// (and the general decoder's 2^11-row transform, skew delta 0 only, after them)
+constexpr uint32_t COL_LGEN = 11;
+constexpr size_t COL_IMG_DWORDS = col_img_offset(COL_LGEN, 0) + ((1u << COL_LGEN) - 1) * 20;
 // n = 2^COL_LMIN .. 2^(COL_LMAX+1): tables of n entries at n - 2^COL_LMIN
 constexpr size_t col_v_offset(uint32_t n) { return n - (1u << COL_LMIN); }
 constexpr size_t COL_V_DWORDS = col_v_offset(4u << COL_LMAX);

@@ -132,8 +132,8 @@ void build(HostTables& t) {
     // j covering rows [j 2^(kb+1), (j+1) 2^(kb+1))) is the twiddle of skew
     // index j 2^(kb+1) + 2^kb + delta - 1 (engine_naive.rs:43-124).
     t.col_img.assign(COL_IMG_DWORDS, 0);
-    for (uint32_t L = COL_LMIN; L <= COL_LMAX; L++)
-        for (uint32_t d = 0; d < 2; d++) {
+    for (uint32_t L = COL_LMIN; L <= COL_LGEN; L++)
+        for (uint32_t d = 0; d < (L == COL_LGEN ? 1u : 2u); d++) {
             const uint32_t N = 1u << L, delta = d ? N : 0;
             uint32_t* img = &t.col_img[col_img_offset(L, d)];
             for (uint32_t g = 0; g + 1 < N; g++) {

@@ -218,10 +218,12 @@ def test_col_decode_check_counts(eng, k, m):
     assert e.value.kind == "InvalidArgument"
 
 
-@pytest.mark.parametrize("k,m", [(100, 100), (300, 300), (200, 256), (50, 60), (512, 512), (33, 64), (700, 300)])
+@pytest.mark.parametrize("k,m", [(100, 100), (300, 300), (200, 256), (50, 60), (512, 512), (33, 64), (700, 300),
+                                 # 2^11 work rows (8-wave workgroups)
+                                 (1000, 1000), (1000, 100), (1024, 1024), (600, 1000), (1500, 500)])
 @pytest.mark.parametrize("pattern", ["1pct", "random", "mixed"])
 def test_col_general_decode(eng, k, m, pattern):
-    """The general decode (any loss pattern) of up to 1024 work rows in one
+    """The general decode (any loss pattern) of up to 2048 work rows in one
     launch: polynomial, gather of both segments, IFFT, formal derivative, FFT,
     reveal (rate_high.rs:168-247); every lost original restored bit for bit,
     received originals untouched."""
