@@ -409,7 +409,7 @@ template <int L, int PTS> __device__ __forceinline__ void col_eval(const ColArgs
         const uint32_t p = t + NT * j;
         const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
         const bool rcv = in_a ? (!a.flags || f[j]) : (in_b && (!a.flags_o || f[j]));
-        x[j] = (in_a || in_b) ? !rcv : (p < a.chunk);
+        x[j] = (in_a || in_b) ? !rcv : (int)(p < a.chunk ? a.e_pad : a.e_tail);
         if (blockIdx.x == 0 && a.rcount) {
             // (below 64 threads a 64-row chunk spans 64 / NT values of j)
             constexpr int PER = NT >= 64 ? 1 : 64 / NT;
@@ -430,7 +430,7 @@ template <int L, int PTS> __device__ __forceinline__ void col_eval(const ColArgs
     for (int j = 0; j < PTS; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
     fwht_points<NT, PTS>(x, sx);
 #pragma unroll
-    for (int j = 0; j < PTS; j++) elds[t + NT * j] = mod65535(x[j]);
+    for (int j = 0; j < PTS; j++) elds[t + NT * j] = mod65535(x[j] + (int)a.e_k);
 }
 
 // The formal derivative (Engine::formal_derivative, src/engine.rs:233-238) of
@@ -524,9 +524,10 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         for (int m = 0; m < 4; m++) {
             const uint32_t r = 4 * t + m;
             rcv[m] = r < a.in_rows && (!a.flags || a.flags[r] != 0);
+            if (GEN && a.rev_a && r < a.in_rows) lost[m] = !rcv[m];  // (low rate: originals = segment A)
             if (GEN && r >= a.chunk && r - a.chunk < a.o_rows) {
                 rcv[m] = !a.flags_o || a.flags_o[r - a.chunk] != 0;
-                lost[m] = !rcv[m];
+                if (!a.rev_a) lost[m] = !rcv[m];
             }
         }
         uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
@@ -739,7 +740,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         }
         const bool st_ok = GEN ? lost[m] : r < a.out_rows;
         if (st_ok) {
-            uint32_t* p = (uint32_t*)(out + (size_t)(GEN ? r - a.chunk : r) * a.S_out);
+            uint32_t* p = (uint32_t*)(out + (size_t)(GEN && !a.rev_a ? r - a.chunk : r) * a.S_out);
             __builtin_nontemporal_store(vl, p);
             __builtin_nontemporal_store(vh, p + 8);
         }

@@ -440,8 +440,8 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // High-rate half decodes of 2^9 / 2^10-row halves through the column
     // codec: it evaluates the polynomial itself (an n-point XOR convolution,
     // rs16_col.hip) and writes rcount; no kernel here.
-    eval_in_col = S && g.high &&
-                  (half_decode(g) ? col_ok(ilog2(g.n) - 1, S, nstripes) : col_ok(ilog2(g.n), S, nstripes, true));
+    eval_in_col = S && (half_decode(g) ? g.high && col_ok(ilog2(g.n) - 1, S, nstripes)
+                                       : col_ok(ilog2(g.n), S, nstripes, true));
     if (eval_in_col) return RS16_OK;
     es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
     hipEvent_t ev;
@@ -548,6 +548,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
             c.base_in = c.skew_ifft = src;
             c.base_out = c.skew_fft = dst;
             c.chunk = g.chunk;
+            c.e_pad = 1;  // (high rate: padding rows erased, nothing above the originals)
             if (col_eval) {
                 // eval_poly in the kernel (decode_eval launched nothing)
                 c.flags_o = flags_b;
@@ -571,9 +572,11 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         RS16_PASS(DEC_HALF_LAST, lo, a, batch((orig + (1u << lo) - 1) >> lo, zs, 0, 0), s);
         return RS16_OK;
     }
-    if (eval_in_col && g.high) {
-        // up to 2^10 work rows: the whole general decode in one launch,
-        // polynomial and formal derivative in the kernel (rs16_col.hip)
+    if (eval_in_col) {
+        // up to 2^11 work rows: the whole general decode in one launch,
+        // polynomial and formal derivative in the kernel (rs16_col.hip);
+        // segment A / B = recovery / originals (high rate) or originals /
+        // recovery (low rate, rate_low.rs:168-247)
         ColArgs c = col_args();
         c.in = seg_a;
         c.flags = flags_a;
@@ -583,13 +586,17 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         c.flags_o = flags_b;
         c.o_rows = g.b_count;
         c.chunk = g.chunk;
+        c.rev_a = g.high ? 0 : 1;
+        c.e_pad = g.high ? 1 : 0;
+        c.e_tail = g.high ? 0 : 1;
+        c.e_k = g.high ? 0 : host_tables().col_k[L];
         c.out = rest;
         c.S_in = c.S_out = S_user;
         c.qrow = (uint32_t)(S / 8);
         c.nstripes = ns;
         c.bs_in = bs_a;
         c.bs_out = bs_rest;
-        c.out_rows = g.b_count;
+        c.out_rows = g.high ? g.b_count : g.a_count;
         c.rcount = (uint32_t*)ws_rcount.p;
         return col(c, L, COL_DEC_GEN, s, err);
     }

@@ -25,6 +25,10 @@ struct HostTables {
     // an n-point XOR convolution (rs16_col.hip): col_v[col_v_offset(n) + k] =
     // n^-1 H_n(W)[k] mod 65535 with W = H_65536(log_walsh).
     std::vector<uint32_t> col_v;
+    // the low rate's erasure vector is 1 from row n on (rate_low.rs:183-197):
+    // rows [0, n) of the polynomial gain col_k[log2 n] = LogWalsh[0] -
+    // sum_{j < n} W[j] mod 65535 (sum over all rows of W = 65536 LogWalsh[0])
+    std::vector<uint32_t> col_k;
 };
 constexpr uint32_t COL_LMIN = 6, COL_LMAX = 10;
 constexpr size_t col_img_offset(uint32_t L, uint32_t d) {
@@ -180,7 +184,12 @@ struct ColArgs {
     uint32_t o_rows;
     const uint32_t* vtab;
     uint32_t* rcount;
-    uint32_t chunk;             // decoder: first row of segment B (the originals)
+    uint32_t chunk;             // decoder: first row of segment B
+    // erasure vector: rows [in_rows, chunk) = e_pad, rows from chunk + o_rows
+    // on = e_tail, and e_k added to every log (low rate: e_pad 0, e_tail 1,
+    // e_k = HostTables::col_k; high rate: 1, 0, 0)
+    uint32_t e_pad, e_tail, e_k;
+    uint32_t rev_a;             // COL_DEC_GEN: the originals are segment A (low rate), else B
     // COL_DEC_GEN: the received originals (segment B rows, stride S_in, stripe stride bs_in_b)
     const uint8_t* in_b;
     uint64_t bs_in_b;

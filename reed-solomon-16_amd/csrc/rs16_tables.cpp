@@ -164,6 +164,16 @@ void build(HostTables& t) {
         };
         auto mod = [](int64_t v) { return (uint32_t)(((v % 65535) + 65535) % 65535); };
         fwht(w.data(), GF_ORDER);
+        t.col_k.assign(COL_LGEN + 2, 0);
+        {
+            int64_t pre = 0;
+            for (uint32_t n = 1, j = 0; n <= (2u << COL_LMAX); n <<= 1) {
+                for (; j < n; j++) pre += mod(w[j]);
+                uint32_t lg = 0;
+                while ((1u << lg) < n) lg++;
+                if (lg < t.col_k.size()) t.col_k[lg] = mod((int64_t)t.log_walsh[0] - pre);
+            }
+        }
         t.col_v.assign(COL_V_DWORDS, 0);
         for (uint32_t n = 1u << COL_LMIN; n <= (2u << COL_LMAX); n <<= 1) {
             std::vector<int64_t> v(n);

@@ -113,3 +113,24 @@ def test_conv_eval_matches_oracle(n, seed):
     want = e.copy()
     O.eval_poly(want, n)
     assert np.array_equal(conv_eval(e, n), want[:n].astype(np.int64) % 65535)
+
+
+@pytest.mark.parametrize("n", [64, 512, 2048])
+def test_conv_eval_low_rate_tail(n):
+    """The low rate's erasure vector is 1 from recovery_end on
+    (rate_low.rs:183-197), past row n too: rows [0, n) of eval_poly are the
+    n-point convolution of e[0, n) plus the constant LogWalsh[0] - sum_{j<n} W[j]
+    (HostTables::col_k)."""
+    rng = np.random.default_rng(n + 11)
+    e = np.zeros(65536, np.uint16)
+    chunk = n // 4
+    e[:chunk // 2] = rng.integers(0, 2, chunk // 2)           # originals, some lost
+    e[chunk: chunk + n // 2] = rng.integers(0, 2, n // 2)     # recovery, some lost
+    e[chunk + n // 2:] = 1                                     # the tail, past n as well
+    want = e.copy()
+    O.eval_poly(want, 65536)
+    lw = O.table("log_walsh").astype(np.int64)
+    w = _fwht_int(lw) % 65535
+    k = (int(lw[0]) - int(w[:n].sum())) % 65535
+    got = (conv_eval(e, n) + k) % 65535
+    assert np.array_equal(got, want[:n].astype(np.int64) % 65535)

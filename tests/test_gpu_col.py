@@ -220,7 +220,9 @@ def test_col_decode_check_counts(eng, k, m):
 
 @pytest.mark.parametrize("k,m", [(100, 100), (300, 300), (200, 256), (50, 60), (512, 512), (33, 64), (700, 300),
                                  # 2^11 work rows (8-wave workgroups)
-                                 (1000, 1000), (1000, 100), (1024, 1024), (600, 1000), (1500, 500)])
+                                 (1000, 1000), (1000, 100), (1024, 1024), (600, 1000), (1500, 500),
+                                 # low rate (originals = segment A, erasure tail of ones)
+                                 (100, 1000), (60, 1000), (200, 700)])
 @pytest.mark.parametrize("pattern", ["1pct", "random", "mixed"])
 def test_col_general_decode(eng, k, m, pattern):
     """The general decode (any loss pattern) of up to 2048 work rows in one
@@ -259,3 +261,26 @@ def test_col_general_decode_matches_pass_codec(eng, no_column):
     finally:
         rs16.set_diagnostics(old)
     assert np.array_equal(got, want) and np.array_equal(got, original)
+
+
+@pytest.mark.parametrize("rate", ["high", "low"])
+@pytest.mark.parametrize("k,m", [(300, 300), (100, 1000), (1000, 100)])
+def test_col_general_decode_rate_api(eng, rate, k, m):
+    """General decodes through the Rate API's work buffer, both rates forced."""
+    sb = 64
+    if not rs16.supports(k, m, rate):
+        pytest.skip("unsupported")
+    original = generate_original(k, sb, 7 * k + m)
+    recovery = O.encode(k, m, original, rate=rate)
+    rng = np.random.default_rng(k * m + len(rate))
+    lost = sorted(rng.choice(k, min(k, m) // 3 + 1, replace=False).tolist())
+    dec = rs16.RateDecoder(k, m, sb, rate, engine=eng)
+    for i in range(k):
+        if i not in lost:
+            dec.add_original_shard(i, original[i])
+    for i in rng.choice(m, len(lost), replace=False).tolist():
+        dec.add_recovery_shard(int(i), recovery[i])
+    with dec.decode() as res:
+        got = dict(res.restored_original_iter())
+    assert sorted(got) == lost
+    assert all(np.array_equal(np.frombuffer(got[i], np.uint8), original[i]) for i in lost)
