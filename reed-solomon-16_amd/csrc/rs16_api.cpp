@@ -850,11 +850,13 @@ extern "C" int rs16_decoder_is_high_rate(const rs16_decoder* d) { return d->high
 // ---------------------------------------------------------------------------
 // Device encode of one stripe (or column slice) with work space Z of
 // work_count x S bytes, on stream s.
+// U: the low-rate encoder's chunk of transformed originals (nullptr: the
+// engine's scratch; column slices on concurrent streams pass their own).
 static int encode_dev(rs16_engine* e, bool high, size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec,
-                      uint8_t* Z, hipStream_t s, rs16_error* err) {
+                      uint8_t* Z, hipStream_t s, rs16_error* err, uint8_t* U = nullptr) {
     if (high && k <= next_pow2(m)) return e->encode_high_fused(k, m, S, S, d_orig, d_rec, Z, s, err);
     return high ? e->encode_high_multi(k, m, S, S, d_orig, d_rec, Z, s, err)
-                : e->encode_low_multi(k, m, S, S, d_orig, d_rec, Z, s, err);
+                : e->encode_low_multi(k, m, S, S, d_orig, d_rec, Z, s, err, U);
 }
 
 extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, const void* d_original,
@@ -964,6 +966,7 @@ extern "C" int rs16_encode_host(rs16_engine* e, size_t k, size_t m, size_t S, co
         RS16_HIP(sl.orig.reserve(k * W));
         RS16_HIP(sl.rec.reserve(m * W));
         RS16_HIP(sl.z.reserve(wc * W));
+        if (!high) RS16_HIP(sl.u.reserve(next_pow2(k) * W));  // (the two slots run concurrently)
     }
     if (int rc = e->host_slots(err)) return rc;
     for (size_t off = 0, j = 0; off < S; off += W, j++) {
@@ -972,7 +975,7 @@ extern "C" int rs16_encode_host(rs16_engine* e, size_t k, size_t m, size_t S, co
         RS16_HIP(hipMemcpy2DAsync(sl.orig.p, w, (const uint8_t*)h_original + off, S, w, k, hipMemcpyHostToDevice,
                                   sl.s));
         if (int rc = encode_dev(e, high, k, m, w, (const uint8_t*)sl.orig.p, (uint8_t*)sl.rec.p, (uint8_t*)sl.z.p,
-                                sl.s, err))
+                                sl.s, err, high ? nullptr : (uint8_t*)sl.u.p))
             return rc;
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_recovery + off, S, sl.rec.p, w, w, m, hipMemcpyDeviceToHost, sl.s));
     }

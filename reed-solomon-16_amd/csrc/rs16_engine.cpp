@@ -718,7 +718,7 @@ int rs16_engine::encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, 
 // are not made: the transformed chunk goes to the scratch U and the FFT's
 // first pass reads it for every chunk (PassArgs::in_rows_mask).
 int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
-                                  uint8_t* Z, hipStream_t s, rs16_error* err) {
+                                  uint8_t* Z, hipStream_t s, rs16_error* err, uint8_t* U) {
     const size_t chunk = next_pow2(k);
     const uint32_t nch = (uint32_t)((m + chunk - 1) / chunk);
     const int L = ilog2(chunk), lo = L <= 8 ? L : L / 2, hi = L - lo;
@@ -741,8 +741,10 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
         c.skew_fft = (uint32_t)chunk;
         return col(c, L, COL_ENC, s, err);
     }
-    RS16_HIP(ws_u.reserve(chunk * S));
-    uint8_t* U = (uint8_t*)ws_u.p;
+    if (!U) {
+        RS16_HIP(ws_u.reserve(chunk * S));
+        U = (uint8_t*)ws_u.p;
+    }
     PassArgs a = base_args(this, S);
     a.seg_a = d_orig;
     a.S_seg = S_user;

@@ -210,8 +210,11 @@ struct rs16_engine {
     // recovery rows [0, m) go to d_rec (pitch S_user; may be Z).
     int encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
                           uint8_t* Z, hipStream_t s, rs16_error* err);
+    // (U: chunk x S bytes for the transformed originals; nullptr = the
+    // engine's ws_u -- callers running several encodes concurrently on other
+    // streams pass their own)
     int encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
-                         uint8_t* Z, hipStream_t s, rs16_error* err);
+                         uint8_t* Z, hipStream_t s, rs16_error* err, uint8_t* U = nullptr);
     int fft_to_recovery(size_t m, size_t S, size_t S_user, const uint8_t* src, uint8_t* Z, uint8_t* d_rec,
                         size_t chunk, uint32_t nch, uint32_t skew, hipStream_t s, rs16_error* err);
 };
