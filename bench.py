@@ -313,7 +313,9 @@ def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
         "gib_s": step_bytes * n4 / t_all / GIB, "ms_per_step": t_all / n4 * 1e3,
         "codec_only_gib_s": step_bytes * n4 / t_codec / GIB, "codec_only_ms": t_codec / n4 * 1e3,
         "collectives_ms": t_coll / n4 * 1e3,
-        "collective_bytes_per_step": 4 * (k * S4 - k * w) if world > 1 else 0,
+        # scatter originals (k rows) + gather recovery (m) + scatter recovery (m)
+        # + gather originals (k), each moving every column but the root's own slice
+        "collective_bytes_per_step": 2 * (k + m) * (S4 - rs16.column_slice(S4, world, 0)[1]) if world > 1 else 0,
         "restored_stripe_verified": ok, "whole_configs4": world == 8}
 
 

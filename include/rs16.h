@@ -335,6 +335,20 @@ int rs16_scatter_columns(rs16_comm* const* comms, int n, int root, size_t rows, 
                          const void* const* d_full, void* const* d_slice, void* stream, rs16_error* err);
 int rs16_gather_columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t shard_bytes,
                         const void* const* d_slice, void* const* d_full, void* stream, rs16_error* err);
+/* Diagnostics: the multi-rank data path of rs16_scatter_columns /
+ * rs16_gather_columns on ONE rank.  `comm` is a one-rank communicator; the
+ * array is split into `vslices` column slices (rs16_column_slice with nranks =
+ * vslices) that are all owned by that rank: slice 0 is the root's own (one
+ * pitched copy), every other slice goes through the staging pack, one grouped
+ * ncclSend / ncclRecv per slice with the rank itself as the peer, and (gather)
+ * the unpack, exactly as another rank's slice would.  d_slices[j] = slice j's
+ * rows x width_j buffer.  No reference counterpart (the reference has no
+ * multi-GPU path); lets a one-GPU machine run the code the driver's 8-GPU
+ * run depends on (tests/test_gpu_rccl.py). */
+int rs16_scatter_columns_virtual(rs16_comm* comm, int vslices, size_t rows, size_t shard_bytes, const void* d_full,
+                                 void* const* d_slices, void* stream, rs16_error* err);
+int rs16_gather_columns_virtual(rs16_comm* comm, int vslices, size_t rows, size_t shard_bytes,
+                                const void* const* d_slices, void* d_full, void* stream, rs16_error* err);
 
 /* ---- Device memory helpers (so FFI callers need no HIP headers) ------- */
 void* rs16_device_alloc(rs16_engine* eng, size_t bytes, rs16_error* err);

@@ -117,15 +117,25 @@ extern "C" int rs16_engine_set_slices(rs16_engine* e, int n, rs16_error* err) {
 // The received counts of the engine's last decode against the device flags
 // (the eval_poly kernels count the received rows per 64-row chunk).
 extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) {
-    if (!e->last_dec_valid) return set_error(err, RS16_OK);
+    if (!e->last_dec_valid && !e->last_dec_flags_only) return set_error(err, RS16_OK);
     if (int rc = e->activate(err)) return rc;
     RS16_HIP(hipStreamSynchronize(e->pick(stream)));
     const DecodeGeom& g = e->last_dec;
-    const size_t chunks = ((size_t)g.n + 63) / 64;
-    std::vector<uint32_t> c(2 * chunks);
-    RS16_HIP(hipMemcpy(c.data(), e->ws_rcount.p, c.size() * 4, hipMemcpyDeviceToHost));
     uint64_t a = 0, b = 0;
-    for (size_t i = 0; i < chunks; i++) a += c[2 * i], b += c[2 * i + 1];
+    if (e->last_dec_flags_only) {
+        // nothing was restored and no kernel counted: count the flags here
+        // (the caller's arrays, as they are now; segment A / B sizes)
+        std::vector<uint8_t> f(std::max(g.a_count, g.b_count));
+        RS16_HIP(hipMemcpy(f.data(), e->last_flags_a, g.a_count, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < g.a_count; i++) a += f[i] != 0;
+        RS16_HIP(hipMemcpy(f.data(), e->last_flags_b, g.b_count, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < g.b_count; i++) b += f[i] != 0;
+    } else {
+        const size_t chunks = ((size_t)g.n + 63) / 64;
+        std::vector<uint32_t> c(2 * chunks);
+        RS16_HIP(hipMemcpy(c.data(), e->ws_rcount.p, c.size() * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < chunks; i++) a += c[2 * i], b += c[2 * i + 1];
+    }
     // (orig_recv, rec_recv) as the caller gave them to rs16_decode_device
     const uint64_t want_o = g.high ? g.b_recv : g.a_recv, want_r = g.high ? g.a_recv : g.b_recv;
     const uint64_t got_o = g.high ? b : a, got_r = g.high ? a : b;
@@ -546,7 +556,9 @@ extern "C" int rs16_encoder_encode(rs16_encoder* enc, rs16_error* err) {
     else if (enc->high)
         rc = e->encode_high_multi(enc->k, enc->m, enc->S, enc->S, w, w, w, e->stream, err);
     else
-        rc = e->encode_low_multi(enc->k, enc->m, enc->S, enc->S, w, w, w, e->stream, err);
+        rc = e->ws_u.reserve(next_pow2(enc->k) * enc->S) == hipSuccess
+                 ? e->encode_low_multi(enc->k, enc->m, enc->S, enc->S, w, w, w, (uint8_t*)e->ws_u.p, e->stream, err)
+                 : hip_fail(err, hipErrorOutOfMemory);
     if (rc) return rc;
     if (int rc2 = e->scratch_done(e->stream, err)) return rc2;
     // a host round gets its results back in one copy, right behind the passes
@@ -781,6 +793,9 @@ static int decoder_fetch(rs16_decoder* d, rs16_error* err) {
 }
 extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
     if (!d->eng || d->decoded) return set_error(err, RS16_INVALID_ARGUMENT);
+    // (the Rate decoder counts its own received set, as the reference does:
+    // there is nothing for rs16_decode_check, which serves rs16_decode_device)
+    d->eng->forget_decode();
     // decode_begin (src/rate/decoder_work.rs:120-139)
     if (d->orig_recv + d->rec_recv < d->k)
         return set_error(err, RS16_NOT_ENOUGH_SHARDS, d->k, d->orig_recv, d->rec_recv);
@@ -808,6 +823,7 @@ extern "C" int rs16_decoder_decode(rs16_decoder* d, rs16_error* err) {
     if (int rc = e->decode_fused(g, d->S, d->S, w, fl, w + (size_t)g.chunk * d->S, fl + GF_ORDER, w + d->orig_base * d->S,
                                  w, (uint8_t*)d->ubuf.p, e->stream, err))
         return rc;
+    e->forget_decode();
     if (int rc = e->scratch_done(e->stream, err)) return rc;
     if (d->host_round)
         if (int rc = decoder_fetch(d, err)) return rc;
@@ -850,13 +866,22 @@ extern "C" int rs16_decoder_is_high_rate(const rs16_decoder* d) { return d->high
 // ---------------------------------------------------------------------------
 // Device encode of one stripe (or column slice) with work space Z of
 // work_count x S bytes, on stream s.
-// U: the low-rate encoder's chunk of transformed originals (nullptr: the
-// engine's scratch; column slices on concurrent streams pass their own).
+// Z: work_count x S, U: next_pow2(k) x S for the low rate (the transformed
+// originals) -- both owned by stream s for the call: the engine's ws_z /
+// ws_u on the engine-ordered paths (order() / scratch_done()), a slot's own
+// buffers on concurrent slots.
 static int encode_dev(rs16_engine* e, bool high, size_t k, size_t m, size_t S, const uint8_t* d_orig, uint8_t* d_rec,
-                      uint8_t* Z, hipStream_t s, rs16_error* err, uint8_t* U = nullptr) {
+                      uint8_t* Z, uint8_t* U, hipStream_t s, rs16_error* err) {
     if (high && k <= next_pow2(m)) return e->encode_high_fused(k, m, S, S, d_orig, d_rec, Z, s, err);
     return high ? e->encode_high_multi(k, m, S, S, d_orig, d_rec, Z, s, err)
-                : e->encode_low_multi(k, m, S, S, d_orig, d_rec, Z, s, err, U);
+                : e->encode_low_multi(k, m, S, S, d_orig, d_rec, Z, U, s, err);
+}
+// The engine's own low-rate scratch for an engine-ordered call.
+static uint8_t* engine_u(rs16_engine* e, bool high, size_t k, size_t S, rs16_error* err, int* rc) {
+    *rc = RS16_OK;
+    if (high) return nullptr;
+    if (hipError_t he = e->ws_u.reserve(next_pow2(k) * S)) return *rc = hip_fail(err, he), nullptr;
+    return (uint8_t*)e->ws_u.p;
 }
 
 extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, const void* d_original,
@@ -870,8 +895,11 @@ extern "C" int rs16_encode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     RS16_HIP(e->ws_z.reserve(wc * S));
     const int n = (high && k <= next_pow2(m)) ? e->slice_count(S) : 1;
     if (n == 1) {
+        int urc;
+        uint8_t* U = engine_u(e, high, k, S, err, &urc);
+        if (urc) return urc;
         if (int rc = encode_dev(e, high, k, m, S, (const uint8_t*)d_original, (uint8_t*)d_recovery,
-                                (uint8_t*)e->ws_z.p, s, err))
+                                (uint8_t*)e->ws_z.p, U, s, err))
             return rc;
         if (int rc = e->scratch_done(s, err)) return rc;
         return set_error(err, RS16_OK);
@@ -922,9 +950,12 @@ extern "C" int rs16_encode_device_batch(rs16_engine* e, size_t k, size_t m, size
             return rc;
     } else {
         RS16_HIP(e->ws_z.reserve(wc * S));
+        int urc;
+        uint8_t* U = engine_u(e, high, k, S, err, &urc);
+        if (urc) return urc;
         for (size_t i = 0; i < nstripes; i++)
             if (int rc = encode_dev(e, high, k, m, S, o + i * original_stride, r + i * recovery_stride,
-                                    (uint8_t*)e->ws_z.p, s, err))
+                                    (uint8_t*)e->ws_z.p, U, s, err))
                 return rc;
     }
     if (int rc = e->scratch_done(s, err)) return rc;
@@ -975,7 +1006,7 @@ extern "C" int rs16_encode_host(rs16_engine* e, size_t k, size_t m, size_t S, co
         RS16_HIP(hipMemcpy2DAsync(sl.orig.p, w, (const uint8_t*)h_original + off, S, w, k, hipMemcpyHostToDevice,
                                   sl.s));
         if (int rc = encode_dev(e, high, k, m, w, (const uint8_t*)sl.orig.p, (uint8_t*)sl.rec.p, (uint8_t*)sl.z.p,
-                                sl.s, err, high ? nullptr : (uint8_t*)sl.u.p))
+                                high ? nullptr : (uint8_t*)sl.u.p, sl.s, err))
             return rc;
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_recovery + off, S, sl.rec.p, w, w, m, hipMemcpyDeviceToHost, sl.s));
     }
@@ -1004,6 +1035,7 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
         RS16_HIP(sl.rec.reserve(m * W));
         RS16_HIP(sl.z.reserve((size_t)g.n * W));
         RS16_HIP(sl.u.reserve((size_t)g.n * W));
+        RS16_HIP(sl.rcount.reserve(GF_ORDER / 64 * 8));
     }
     // received flags -> device; erasure logs once, shared by every slice
     if (int rc = e->order(e->stream, err)) return rc;
@@ -1028,13 +1060,15 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
         const uint8_t* o = (const uint8_t*)sl.orig.p;
         const uint8_t* r = (const uint8_t*)sl.rec.p;
         if (int rc = e->decode_passes(g, w, w, high ? r : o, fa, high ? o : r, fb, (uint8_t*)sl.orig.p,
-                                      (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, sl.s, err))
+                                      (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, (uint32_t*)sl.rcount.p, sl.s, err))
             return rc;
         // restored originals land in place; received rows come back unchanged
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_original + off, S, sl.orig.p, w, w, k, hipMemcpyDeviceToHost, sl.s));
     }
     for (auto& sl : e->hslot) RS16_HIP(hipStreamSynchronize(sl.s));
     if (int rc = e->scratch_done(e->stream, err)) return rc;
+    // (the counts came from the host flags themselves: nothing for rs16_decode_check)
+    e->forget_decode();
     return set_error(err, RS16_OK);
 }
 
@@ -1081,10 +1115,11 @@ extern "C" int rs16_encode_host_multi(rs16_engine* const* engines, int n, size_t
         RS16_HIP(sl.orig.reserve(k * w));
         RS16_HIP(sl.rec.reserve(m * w));
         RS16_HIP(sl.z.reserve(wc * w));
+        if (!high) RS16_HIP(sl.u.reserve(next_pow2(k) * w));
         RS16_HIP(hipMemcpy2DAsync(sl.orig.p, w, (const uint8_t*)h_original + off, S, w, k, hipMemcpyHostToDevice,
                                   e->stream));
         if (int rc = encode_dev(e, high, k, m, w, (const uint8_t*)sl.orig.p, (uint8_t*)sl.rec.p, (uint8_t*)sl.z.p,
-                                e->stream, err))
+                                high ? nullptr : (uint8_t*)sl.u.p, e->stream, err))
             return rc;
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_recovery + off, S, sl.rec.p, w, w, m, hipMemcpyDeviceToHost,
                                   e->stream));
@@ -1119,6 +1154,7 @@ extern "C" int rs16_decode_host_multi(rs16_engine* const* engines, int n, size_t
         RS16_HIP(sl.rec.reserve(m * w));
         RS16_HIP(sl.z.reserve((size_t)g.n * w));
         RS16_HIP(sl.u.reserve((size_t)g.n * w));
+        RS16_HIP(sl.rcount.reserve(GF_ORDER / 64 * 8));
         RS16_HIP(e->hflags.reserve(k + m));
         uint8_t* d_of = (uint8_t*)e->hflags.p;
         uint8_t* d_rf = d_of + k;
@@ -1136,13 +1172,24 @@ extern "C" int rs16_decode_host_multi(rs16_engine* const* engines, int n, size_t
         const uint8_t* o = (const uint8_t*)sl.orig.p;
         const uint8_t* r = (const uint8_t*)sl.rec.p;
         if (int rc = e->decode_passes(g, w, w, high ? r : o, fa, high ? o : r, fb, (uint8_t*)sl.orig.p,
-                                      (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, e->stream, err))
+                                      (uint8_t*)sl.z.p, (uint8_t*)sl.u.p, (uint32_t*)sl.rcount.p, e->stream, err))
             return rc;
         RS16_HIP(hipMemcpy2DAsync((uint8_t*)h_original + off, S, sl.orig.p, w, w, k, hipMemcpyDeviceToHost,
                                   e->stream));
     }
     if (int rc = multi_sync(engines, n, err)) return rc;
+    for (int j = 0; j < n; j++) engines[j]->forget_decode();  // (host flags: nothing to check)
     return set_error(err, RS16_OK);
+}
+
+// A decode with nothing to restore (every original received) launches no
+// kernel that counts the flags: remember them, rs16_decode_check reads them.
+static void note_flags_only(rs16_engine* e, const DecodeGeom& g, const uint8_t* fl_a, const uint8_t* fl_b) {
+    e->forget_decode();
+    e->last_dec = g;
+    e->last_flags_a = fl_a;
+    e->last_flags_b = fl_b;
+    e->last_dec_flags_only = true;
 }
 
 extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, void* d_original,
@@ -1151,30 +1198,31 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
                                   rs16_error* err) {
     bool high;
     if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    e->forget_decode();  // (whatever happens below, the previous decode is not checked again)
     if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
     if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
-    if (orig_recv == k) return set_error(err, RS16_OK);
-    if (int rc = e->activate(err)) return rc;
-    hipStream_t s = e->pick(stream);
-    if (int rc = e->order(s, err)) return rc;
     DecodeGeom g = decode_geom(high, k, m);
     g.a_recv = high ? rec_recv : orig_recv;
     g.b_recv = high ? orig_recv : rec_recv;
+    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
+    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
+    if (orig_recv == k) return note_flags_only(e, g, fl_a, fl_b), set_error(err, RS16_OK);
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
     RS16_HIP(e->ws_z.reserve((size_t)g.n * S));
     RS16_HIP(e->ws_u.reserve((size_t)g.n * S));
     const uint8_t* orig = (const uint8_t*)d_original;
     const uint8_t* rec = (const uint8_t*)d_recovery;
     const uint8_t* seg_a = high ? rec : orig;
     const uint8_t* seg_b = high ? orig : rec;
-    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
-    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
     // erasure logs once, then the passes per column slice on the slice streams
     // (one slice: the column codec may compute them itself, decode_eval)
     const int n = e->slice_count(S);
     if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, n == 1 ? S : 0)) return rc;
     if (n == 1) {
         if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
-                                      (uint8_t*)e->ws_u.p, s, err))
+                                      (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, s, err))
             return rc;
         if (int rc = e->scratch_done(s, err)) return rc;
         return set_error(err, RS16_OK);
@@ -1183,9 +1231,11 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     const size_t blocks = S / 64;
     for (int j = 0, b0 = 0; j < n; j++) {
         const size_t b1 = blocks * (j + 1) / n, off = b0 * 64, w = (b1 - b0) * 64;
+        // (decode_eval was told the slices are narrower than S: no column
+        // decode evaluates the polynomial itself, nothing writes rcount here)
         if (int rc = e->decode_passes(g, w, S, seg_a + off, fl_a, seg_b + off, fl_b, (uint8_t*)d_original + off,
                                       (uint8_t*)e->ws_z.p + (size_t)g.n * off, (uint8_t*)e->ws_u.p + (size_t)g.n * off,
-                                      e->sl_stream[j], err))
+                                      nullptr, e->sl_stream[j], err))
             return rc;
         b0 = (int)b1;
     }
@@ -1206,9 +1256,18 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
                                         void* stream, rs16_error* err) {
     bool high;
     if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    e->forget_decode();
     if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
     if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
-    if (nstripes == 0 || orig_recv == k) return set_error(err, RS16_OK);
+    if (nstripes == 0) return set_error(err, RS16_OK);
+    if (orig_recv == k) {
+        DecodeGeom g0 = decode_geom(high, k, m);
+        g0.a_recv = high ? rec_recv : orig_recv;
+        g0.b_recv = high ? orig_recv : rec_recv;
+        note_flags_only(e, g0, high ? d_recovery_received : d_original_received,
+                        high ? d_original_received : d_recovery_received);
+        return set_error(err, RS16_OK);
+    }
     if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S || original_stride % 64 ||
         recovery_stride % 64 || nstripes > ((size_t)1 << 20))
         return set_error(err, RS16_INVALID_ARGUMENT);
@@ -1229,7 +1288,8 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
     const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
     if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, S, nstripes)) return rc;
     if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
-                                  (uint8_t*)e->ws_u.p, s, err, nstripes, bs_a, bs_b, original_stride))
+                                  (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, s, err, nstripes, bs_a, bs_b,
+                                  original_stride))
         return rc;
     if (int rc = e->scratch_done(s, err)) return rc;
     return set_error(err, RS16_OK);

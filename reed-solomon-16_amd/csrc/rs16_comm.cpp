@@ -33,6 +33,10 @@ struct rs16_comm {
     int nranks = 0, rank = 0;
     bool blocking = false;  // ncclCommInitAll communicators are blocking
     DevBuf stage;  // root: packed column slices
+    // the last collective's use of `stage` (recorded on its stream): the
+    // next collective, on whatever stream, waits for it before repacking
+    hipEvent_t stage_ev = nullptr;
+    bool stage_busy = false;
 };
 
 static int nccl_fail(rs16_error* err, ncclResult_t r) { return set_error(err, RS16_DEVICE_ERROR, 1000 + (uint64_t)r); }
@@ -47,20 +51,29 @@ static int nccl_fail(rs16_error* err, ncclResult_t r) { return set_error(err, RS
 // with a deadline, so a rank that never joins makes the others fail with an
 // error (the communicator aborted) instead of hanging the process.
 static constexpr double INIT_DEADLINE_S = 120.0, GROUP_DEADLINE_S = 60.0;
+// On any failure the communicator is aborted here (and must not be used or
+// destroyed again by the caller).
 static ncclResult_t settle(ncclComm_t c, ncclResult_t r, double deadline_s) {
-    if (r != ncclSuccess && r != ncclInProgress) return r;
     const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
+    while (r == ncclInProgress || r == ncclSuccess) {
         ncclResult_t st = ncclSuccess;
-        ncclResult_t q = ncclCommGetAsyncError(c, &st);
-        if (q != ncclSuccess) return q;
-        if (st != ncclInProgress) return st;
+        const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+        if (q != ncclSuccess) {
+            r = q;
+            break;
+        }
+        if (st != ncclInProgress) {
+            r = st;
+            break;
+        }
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > deadline_s) {
-            (void)ncclCommAbort(c);
-            return ncclSystemError;
+            r = ncclSystemError;
+            break;
         }
         std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
+    if (r != ncclSuccess) (void)ncclCommAbort(c);
+    return r;
 }
 
 // Column slice of rank r of n (B = S / 64 blocks).
@@ -89,7 +102,7 @@ extern "C" rs16_comm* rs16_comm_new(rs16_engine* eng, int nranks, int rank, cons
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
     ncclResult_t r = ncclCommInitRankConfig(&c->nc, nranks, u, rank, &cfg);
-    if (c->nc) r = settle(c->nc, r, INIT_DEADLINE_S);
+    if (c->nc) r = settle(c->nc, r, INIT_DEADLINE_S);  // (aborts c->nc on failure)
     if (r != ncclSuccess) {
         c->nc = nullptr;  // (aborted, or never created)
         delete c;
@@ -113,7 +126,14 @@ extern "C" int rs16_comm_init_all(rs16_engine* const* engines, int n, rs16_comm*
     RS16_NCCL(ncclCommInitAll(nc.data(), n, devs.data()));
     for (int i = 0; i < n; i++) {
         comms[i] = new (std::nothrow) rs16_comm();
-        if (!comms[i]) return set_error(err, RS16_INVALID_ARGUMENT);
+        if (!comms[i]) {
+            // nothing half-made survives: every communicator destroyed, every object freed
+            for (int j = 0; j < n; j++) (void)ncclCommDestroy(nc[j]);
+            for (int j = 0; j < i; j++) delete comms[j], comms[j] = nullptr;
+            return set_error(err, RS16_INVALID_ARGUMENT);
+        }
+    }
+    for (int i = 0; i < n; i++) {
         comms[i]->eng = engines[i];
         comms[i]->nc = nc[i];
         comms[i]->nranks = n;
@@ -128,8 +148,11 @@ extern "C" void rs16_comm_free(rs16_comm* c) {
     if (c->eng) {
         (void)hipSetDevice(c->eng->device);
         (void)hipStreamSynchronize(c->eng->stream);
+        // (a collective on a caller's stream: its last use of the staging buffer)
+        if (c->stage_busy) (void)hipEventSynchronize(c->stage_ev);
     }
     if (c->nc) (void)ncclCommDestroy(c->nc);
+    if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
     c->stage.release();
     delete c;
 }
@@ -142,71 +165,92 @@ extern "C" int rs16_column_slice(size_t shard_bytes, int nranks, int rank, size_
     return RS16_OK;
 }
 
-// The root's rows x S array <-> every rank's rows x w_r column slice.
-// d_full[i] / d_slice[i] belong to comms[i] (d_full only read / written on the root).
+// The root's rows x S array <-> P column slices, slice j owned by rank
+// owner(j).  Normally P = nranks and slice j belongs to rank j; d_full[i] /
+// d_slice[i] belong to comms[i] (d_full only read / written on the root).
+// Diagnostic virtual slices (vslices = P > 0, a one-rank communicator): all P
+// slices are owned by rank 0 itself, d_slice[j] is slice j's buffer, and
+// every slice but slice 0 goes through the same staging pack, grouped
+// ncclSend / ncclRecv (to the rank itself) and unpack as another rank's slice
+// would -- so the multi-rank data path runs on a one-GPU machine
+// (tests/test_gpu_rccl.py).
 static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t S, void* const* d_full,
-                   void* const* d_slice, void* stream, bool scatter, rs16_error* err) {
+                   void* const* d_slice, void* stream, bool scatter, rs16_error* err, int vslices = 0) {
     if (!comms || n < 1 || (S % 64) || S == 0) return set_error(err, RS16_INVALID_ARGUMENT);
     const int nranks = comms[0]->nranks;
     if (root < 0 || root >= nranks) return set_error(err, RS16_INVALID_ARGUMENT);
     for (int i = 0; i < n; i++)
         if (!comms[i] || !comms[i]->nc || comms[i]->nranks != nranks) return set_error(err, RS16_INVALID_ARGUMENT);
+    const bool virt = vslices > 0;
+    if (virt && (nranks != 1 || n != 1 || vslices > 4096)) return set_error(err, RS16_INVALID_ARGUMENT);
+    const int P = virt ? vslices : nranks;
+    auto owner = [&](int j) { return virt ? 0 : j; };
+    // the slice that the root keeps without RCCL: its own (slice 0 when virtual)
+    const int own = virt ? 0 : root;
+    // buffer of slice j on local communicator i (which owns it)
+    auto slice_buf = [&](int i, int j) { return virt ? d_slice[j] : d_slice[i]; };
     auto strm = [&](rs16_comm* c) { return (n == 1 && stream) ? (hipStream_t)stream : c->eng->stream; };
-    // root: its own slice directly; scatter: pack the other ranks' slices
-    // (one pitched copy per rank)
+    // root: its own slice directly; scatter: pack every other slice (one
+    // pitched copy each)
     for (int i = 0; i < n; i++) {
         rs16_comm* c = comms[i];
         if (c->rank != root) continue;
         if (int rc = c->eng->activate(err)) return rc;
         size_t off, w;
-        col_slice(S, nranks, root, &off, &w);
+        col_slice(S, P, own, &off, &w);
         if (w && scatter)
-            RS16_HIP(hipMemcpy2DAsync(d_slice[i], w, (const uint8_t*)d_full[i] + off, S, w, rows,
+            RS16_HIP(hipMemcpy2DAsync(slice_buf(i, own), w, (const uint8_t*)d_full[i] + off, S, w, rows,
                                       hipMemcpyDeviceToDevice, strm(c)));
         if (w && !scatter)
-            RS16_HIP(hipMemcpy2DAsync((uint8_t*)d_full[i] + off, S, d_slice[i], w, w, rows, hipMemcpyDeviceToDevice,
-                                      strm(c)));
-        if (nranks == 1) continue;
-        RS16_HIP(c->stage.reserve(rows * S));
+            RS16_HIP(hipMemcpy2DAsync((uint8_t*)d_full[i] + off, S, slice_buf(i, own), w, w, rows,
+                                      hipMemcpyDeviceToDevice, strm(c)));
+        if (P == 1) continue;
+        // the previous collective's use of the staging buffer (maybe on another stream)
+        if (c->stage_busy) RS16_HIP(hipStreamWaitEvent(strm(c), c->stage_ev, 0));
+        if (c->stage.cap < rows * S) {
+            RS16_HIP(hipStreamSynchronize(strm(c)));  // (reserve frees the old buffer)
+            RS16_HIP(c->stage.reserve(rows * S));
+        }
         if (scatter)
-            for (int r = 0; r < nranks; r++) {
-                col_slice(S, nranks, r, &off, &w);
-                if (!w || r == root) continue;
+            for (int j = 0; j < P; j++) {
+                col_slice(S, P, j, &off, &w);
+                if (!w || j == own) continue;
                 RS16_HIP(hipMemcpy2DAsync((uint8_t*)c->stage.p + rows * off, w, (const uint8_t*)d_full[i] + off, S, w,
                                           rows, hipMemcpyDeviceToDevice, strm(c)));
             }
     }
-    if (nranks == 1) return set_error(err, RS16_OK);
+    if (P == 1) return set_error(err, RS16_OK);
     RS16_NCCL(ncclGroupStart());
+    auto p2p = [&](bool send, void* p, size_t bytes, int peer, rs16_comm* c) -> int {
+        const ncclResult_t x = send ? ncclSend(p, bytes, ncclUint8, peer, c->nc, strm(c))
+                                    : ncclRecv(p, bytes, ncclUint8, peer, c->nc, strm(c));
+        if (x != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return nccl_fail(err, x);
+        }
+        return RS16_OK;
+    };
     for (int i = 0; i < n; i++) {
         rs16_comm* c = comms[i];
         if (int rc = c->eng->activate(err)) {
             (void)ncclGroupEnd();
             return rc;
         }
-        size_t off, w;
-        col_slice(S, nranks, c->rank, &off, &w);
-        if (c->rank == root) {
-            for (int r = 0; r < nranks; r++) {
+        // the root's side: one send (scatter) / receive (gather) per slice it does not keep
+        if (c->rank == root)
+            for (int j = 0; j < P; j++) {
                 size_t o2, w2;
-                col_slice(S, nranks, r, &o2, &w2);
-                if (!w2 || r == root) continue;
-                uint8_t* p = (uint8_t*)c->stage.p + rows * o2;
-                ncclResult_t x = scatter ? ncclSend(p, rows * w2, ncclUint8, r, c->nc, strm(c))
-                                         : ncclRecv(p, rows * w2, ncclUint8, r, c->nc, strm(c));
-                if (x != ncclSuccess) {
-                    (void)ncclGroupEnd();
-                    return nccl_fail(err, x);
-                }
+                col_slice(S, P, j, &o2, &w2);
+                if (!w2 || j == own) continue;
+                if (int rc = p2p(scatter, (uint8_t*)c->stage.p + rows * o2, rows * w2, owner(j), c)) return rc;
             }
-        }
-        if (w && c->rank != root) {
-            ncclResult_t x = scatter ? ncclRecv(d_slice[i], rows * w, ncclUint8, root, c->nc, strm(c))
-                                     : ncclSend(d_slice[i], rows * w, ncclUint8, root, c->nc, strm(c));
-            if (x != ncclSuccess) {
-                (void)ncclGroupEnd();
-                return nccl_fail(err, x);
-            }
+        // the owners' side: every slice of this rank that the root does not keep
+        for (int j = 0; j < P; j++) {
+            if (owner(j) != c->rank || j == own) continue;
+            size_t o2, w2;
+            col_slice(S, P, j, &o2, &w2);
+            if (!w2) continue;
+            if (int rc = p2p(!scatter, slice_buf(i, j), rows * w2, root, c)) return rc;
         }
     }
     {
@@ -219,20 +263,24 @@ static int columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t
             }
         }
     }
-    // root, gather: unpack into the full rows x S array
-    if (!scatter)
-        for (int i = 0; i < n; i++) {
-            rs16_comm* c = comms[i];
-            if (c->rank != root) continue;
-            if (int rc = c->eng->activate(err)) return rc;
-            for (int r = 0; r < nranks; r++) {
+    // root, gather: unpack into the full rows x S array; then mark the
+    // staging buffer's last use (both directions)
+    for (int i = 0; i < n; i++) {
+        rs16_comm* c = comms[i];
+        if (c->rank != root) continue;
+        if (int rc = c->eng->activate(err)) return rc;
+        if (!scatter)
+            for (int j = 0; j < P; j++) {
                 size_t off, w;
-                col_slice(S, nranks, r, &off, &w);
-                if (!w || r == root) continue;
+                col_slice(S, P, j, &off, &w);
+                if (!w || j == own) continue;
                 RS16_HIP(hipMemcpy2DAsync((uint8_t*)d_full[i] + off, S, (const uint8_t*)c->stage.p + rows * off, w, w,
                                           rows, hipMemcpyDeviceToDevice, strm(c)));
             }
-        }
+        if (!c->stage_ev) RS16_HIP(hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming));
+        RS16_HIP(hipEventRecord(c->stage_ev, strm(c)));
+        c->stage_busy = true;
+    }
     return set_error(err, RS16_OK);
 }
 
@@ -243,4 +291,19 @@ extern "C" int rs16_scatter_columns(rs16_comm* const* comms, int n, int root, si
 extern "C" int rs16_gather_columns(rs16_comm* const* comms, int n, int root, size_t rows, size_t shard_bytes,
                                    const void* const* d_slice, void* const* d_full, void* stream, rs16_error* err) {
     return columns(comms, n, root, rows, shard_bytes, d_full, (void* const*)d_slice, stream, false, err);
+}
+
+// Diagnostics (include/rs16.h): the multi-rank data path with `vslices`
+// virtual slices, all owned by the one rank of `comm`.
+extern "C" int rs16_scatter_columns_virtual(rs16_comm* comm, int vslices, size_t rows, size_t shard_bytes,
+                                            const void* d_full, void* const* d_slices, void* stream,
+                                            rs16_error* err) {
+    if (!comm || vslices < 1 || !d_slices) return set_error(err, RS16_INVALID_ARGUMENT);
+    void* full = (void*)d_full;
+    return columns(&comm, 1, 0, rows, shard_bytes, &full, d_slices, stream, true, err, vslices);
+}
+extern "C" int rs16_gather_columns_virtual(rs16_comm* comm, int vslices, size_t rows, size_t shard_bytes,
+                                           const void* const* d_slices, void* d_full, void* stream, rs16_error* err) {
+    if (!comm || vslices < 1 || !d_slices) return set_error(err, RS16_INVALID_ARGUMENT);
+    return columns(&comm, 1, 0, rows, shard_bytes, &d_full, (void* const*)d_slices, stream, false, err, vslices);
 }

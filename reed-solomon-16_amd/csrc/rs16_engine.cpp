@@ -401,7 +401,7 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, size_t S_user, cons
                               const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                               hipStream_t s, rs16_error* err) {
     if (int rc = decode_eval(g, flags_a, flags_b, s, err, S)) return rc;
-    return decode_passes(g, S, S_user, seg_a, flags_a, seg_b, flags_b, rest, Z, U, s, err);
+    return decode_passes(g, S, S_user, seg_a, flags_a, seg_b, flags_b, rest, Z, U, (uint32_t*)ws_rcount.p, s, err);
 }
 
 // Erasure logs e = eval_poly(erasure vector) into ws_elog (2-3 small kernels).
@@ -485,7 +485,8 @@ bool rs16_engine::half_decode(const DecodeGeom& g) {
 // ws_work32 (erasure logs), ws_rbits (received rows) and ws_zflag (zero tiles).
 int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                                const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
-                               hipStream_t s, rs16_error* err, size_t nst, size_t bs_a, size_t bs_b, size_t bs_rest) {
+                               uint32_t* rcount, hipStream_t s, rs16_error* err, size_t nst, size_t bs_a, size_t bs_b,
+                               size_t bs_rest) {
     PassArgs a = base_args(this, S);
     a.S_seg = a.S_rest = S_user;
     a.seg_a = seg_a;
@@ -554,7 +555,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
                 c.flags_o = flags_b;
                 c.o_rows = g.b_count;
                 c.vtab = nullptr;  // (col(): d_col_v + col_v_offset(2^(L+1)))
-                c.rcount = (uint32_t*)ws_rcount.p;
+                c.rcount = rcount;
                 return col(c, Lh, COL_DEC_EVAL, s, err);
             }
             c.elog = (const uint32_t*)ws_work32.p;  // (eval_poly without its last H_lo: elog_fused)
@@ -597,7 +598,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         c.bs_in = bs_a;
         c.bs_out = bs_rest;
         c.out_rows = g.high ? g.b_count : g.a_count;
-        c.rcount = (uint32_t*)ws_rcount.p;
+        c.rcount = rcount;
         return col(c, L, COL_DEC_GEN, s, err);
     }
     if (L <= 8) {
@@ -718,7 +719,7 @@ int rs16_engine::encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, 
 // are not made: the transformed chunk goes to the scratch U and the FFT's
 // first pass reads it for every chunk (PassArgs::in_rows_mask).
 int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
-                                  uint8_t* Z, hipStream_t s, rs16_error* err, uint8_t* U) {
+                                  uint8_t* Z, uint8_t* U, hipStream_t s, rs16_error* err) {
     const size_t chunk = next_pow2(k);
     const uint32_t nch = (uint32_t)((m + chunk - 1) / chunk);
     const int L = ilog2(chunk), lo = L <= 8 ? L : L / 2, hi = L - lo;
@@ -741,10 +742,9 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
         c.skew_fft = (uint32_t)chunk;
         return col(c, L, COL_ENC, s, err);
     }
-    if (!U) {
-        RS16_HIP(ws_u.reserve(chunk * S));
-        U = (uint8_t*)ws_u.p;
-    }
+    // U belongs to the caller's stream (no engine-wide fallback: two calls
+    // on concurrent streams sharing one buffer restored wrong data, round 3)
+    if (!U) return set_error(err, RS16_INVALID_ARGUMENT);
     PassArgs a = base_args(this, S);
     a.seg_a = d_orig;
     a.S_seg = S_user;

@@ -87,6 +87,13 @@ struct rs16_engine {
     // the last decode's geometry and the received counts it was given (rs16_decode_check)
     rs16::DecodeGeom last_dec{};
     bool last_dec_valid = false;
+    // ... or, when that decode had nothing to restore (every original
+    // received: no kernel counted anything), its device flag arrays, which
+    // rs16_decode_check then reads back and counts itself
+    const uint8_t* last_flags_a = nullptr;
+    const uint8_t* last_flags_b = nullptr;
+    bool last_dec_flags_only = false;
+    void forget_decode() { last_dec_valid = last_dec_flags_only = false; }
     // Host-resident pipeline (rs16_encode_host / rs16_decode_host): column
     // slices alternate between two slots, each with its own stream and the
     // device buffers of one slice, so copies and compute of different slices
@@ -95,6 +102,7 @@ struct rs16_engine {
     struct HostSlot {
         hipStream_t s = nullptr;
         rs16::DevBuf orig, rec, z, u;
+        rs16::DevBuf rcount;  // the slot's column decodes' received counts (never ws_rcount)
     };
     HostSlot hslot[2];
     // Column slices of the device-resident one-shot codec: a stripe's shard
@@ -188,10 +196,13 @@ struct rs16_engine {
     // decode it computes eval_poly itself and no kernel is launched here.
     int decode_eval(const rs16::DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
                     rs16_error* err, size_t S = 0, size_t nstripes = 1);
+    // rcount: where a column decode that evaluates the polynomial itself
+    // writes the received counts (ErasureSpec::rcount layout): ws_rcount on
+    // the call's own stream, a buffer of their own for concurrent slots.
     int decode_passes(const rs16::DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                       const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
-                      hipStream_t s, rs16_error* err, size_t nstripes = 1, size_t bs_a = 0, size_t bs_b = 0,
-                      size_t bs_rest = 0);
+                      uint32_t* rcount, hipStream_t s, rs16_error* err, size_t nstripes = 1, size_t bs_a = 0,
+                      size_t bs_b = 0, size_t bs_rest = 0);
     // The half-transform decode applies (every original lost, originals
     // segment = one half of the work rows).
     static bool half_decode(const rs16::DecodeGeom& g);
@@ -210,11 +221,11 @@ struct rs16_engine {
     // recovery rows [0, m) go to d_rec (pitch S_user; may be Z).
     int encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
                           uint8_t* Z, hipStream_t s, rs16_error* err);
-    // (U: chunk x S bytes for the transformed originals; nullptr = the
-    // engine's ws_u -- callers running several encodes concurrently on other
-    // streams pass their own)
+    // U: chunk x S bytes for the transformed originals, owned by the call's
+    // stream (the engine's ws_u on the engine-ordered paths, a slot's own
+    // buffer on concurrent slots); required -- there is no fallback.
     int encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
-                         uint8_t* Z, hipStream_t s, rs16_error* err, uint8_t* U = nullptr);
+                         uint8_t* Z, uint8_t* U, hipStream_t s, rs16_error* err);
     int fft_to_recovery(size_t m, size_t S, size_t S_user, const uint8_t* src, uint8_t* Z, uint8_t* d_rec,
                         size_t chunk, uint32_t nch, uint32_t skew, hipStream_t s, rs16_error* err);
 };

@@ -782,3 +782,19 @@ def gather_columns(comms, root, rows, shard_bytes, d_slice, d_full, stream=None)
     err = RS16Error()
     _check(lib().rs16_gather_columns((C.c_void_p * len(comms))(*[c.h for c in comms]), len(comms), root, rows,
                                      shard_bytes, _ptrs(d_slice), _ptrs(d_full), stream, C.byref(err)), err)
+
+
+def scatter_columns_virtual(comm, vslices, rows, shard_bytes, d_full, d_slices, stream=None):
+    """Diagnostics: the multi-rank scatter on one rank -- `vslices` column
+    slices all owned by comm's only rank, every slice but slice 0 through the
+    staging pack and a grouped ncclSend / ncclRecv to the rank itself."""
+    err = RS16Error()
+    _check(lib().rs16_scatter_columns_virtual(comm.h, vslices, rows, shard_bytes, int(d_full), _ptrs(d_slices),
+                                              stream, C.byref(err)), err)
+
+
+def gather_columns_virtual(comm, vslices, rows, shard_bytes, d_slices, d_full, stream=None):
+    """Diagnostics: the mirror image of scatter_columns_virtual (slices -> d_full)."""
+    err = RS16Error()
+    _check(lib().rs16_gather_columns_virtual(comm.h, vslices, rows, shard_bytes, _ptrs(d_slices), int(d_full),
+                                             stream, C.byref(err)), err)

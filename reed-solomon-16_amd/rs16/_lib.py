@@ -100,6 +100,8 @@ SIGNATURES = {
     "rs16_column_slice": (_i, [_sz, _i, _i, C.POINTER(_sz), C.POINTER(_sz)]),
     "rs16_scatter_columns": (_i, [_p, _i, _i, _sz, _sz, _p, _p, _p, _e]),
     "rs16_gather_columns": (_i, [_p, _i, _i, _sz, _sz, _p, _p, _p, _e]),
+    "rs16_scatter_columns_virtual": (_i, [_p, _i, _sz, _sz, _p, _p, _p, _e]),
+    "rs16_gather_columns_virtual": (_i, [_p, _i, _sz, _sz, _p, _p, _p, _e]),
     "rs16_encode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _e]),
     "rs16_decode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _p, _p, _e]),
     "rs16_stream_create": (_p, [_p, _e]),

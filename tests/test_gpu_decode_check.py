@@ -45,3 +45,28 @@ def test_counts_checked(k, m, sb, unaligned):
         rs16.decode_device(k, m, sb, d_x.ptr, d_fo.ptr + pad, d_r.ptr, d_fr.ptr + pad, int(om.sum()) - 1,
                            int(rm.sum()) + 1, engine=eng, check=True)
     assert e.value.kind == "InvalidArgument"
+
+
+@pytest.mark.parametrize("k,m", [(1000, 1000), (100, 300)])
+def test_counts_checked_nothing_to_restore(k, m):
+    # a decode whose counts claim every original was received
+    # returns without a kernel; the checked mode still compares the counts
+    # with the flags (read back) instead of the previous decode's counts
+    eng = rs16.default_engine()
+    sb = 64
+    orig = generate_original(k, sb, 5)
+    d_o, d_r = DeviceArray.from_numpy(eng, orig), DeviceArray(eng, m * sb)
+    rs16.encode_device(k, m, sb, d_o.ptr, d_r.ptr, engine=eng)
+    om = np.ones(k, np.uint8)
+    rm = np.zeros(m, np.uint8)
+    rm[:3] = 1
+    d_fo, d_fr = DeviceArray.from_numpy(eng, om), DeviceArray.from_numpy(eng, rm)
+    # a correct "nothing to do" decode: OK
+    rs16.decode_device(k, m, sb, d_o.ptr, d_fo.ptr, d_r.ptr, d_fr.ptr, k, 3, engine=eng, check=True)
+    # the flags say 3 originals are lost, the counts say none: detected
+    om[[0, 7, k - 1]] = 0
+    d_fo.upload(om)
+    with pytest.raises(rs16.Error) as e:
+        rs16.decode_device(k, m, sb, d_o.ptr, d_fo.ptr, d_r.ptr, d_fr.ptr, k, 3, engine=eng, check=True)
+    assert e.value.kind == "InvalidArgument"
+    assert np.array_equal(d_o.download(shape=(k, sb)), orig)  # nothing written

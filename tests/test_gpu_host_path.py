@@ -55,3 +55,33 @@ def test_host_decode_errors(eng):
                          np.array([1, 0], np.uint8), engine=eng)
     assert e.value == rs16.Error("NotEnoughShards", original_count=4, original_received_count=2,
                                  recovery_received_count=1)
+
+
+# Scratch ownership of the two host slots: every slot
+# runs its slices on its own stream with its own work buffers -- the low-rate
+# multi-chunk encoder's transformed originals (U) and the column decoder's
+# received counts included; nothing falls back to engine-wide scratch.  Many
+# narrow slices (>= 4 per slot) make the two slots overlap for most of the
+# call; results must equal the oracle's bit for bit, every time.
+@pytest.mark.parametrize("k,m,sb,slice_bytes,loss", [
+    (300, 3000, 1024, 128, "all"),    # low rate, 6 recovery chunks of 512 (encode_low_multi per slot)
+    (1000, 1000, 1024, 128, "1pct"),  # general decode of 2^11 work rows: column codec, polynomial in the kernel
+    (100, 1000, 512, 64, "1pct"),     # low-rate column general decode (n = 2^11 rows)
+    (1000, 1000, 1024, 64, "all"),    # half-transform column decode, 16 slices
+])
+def test_host_slots_own_scratch(eng, k, m, sb, slice_bytes, loss):
+    original = generate_original(k, sb, 11)
+    want = O.encode(k, m, original)
+    for rep in range(3):
+        hrec = np.zeros((m, sb), np.uint8)
+        rs16.encode_host(k, m, sb, original, hrec, slice_bytes, engine=eng)
+        assert np.array_equal(hrec, want), f"encode, repetition {rep}"
+        L = min(k, m) if loss == "all" else max(1, min(k, m) // 100)
+        of = np.ones(k, np.uint8)
+        of[k - L:] = 0
+        rf = np.zeros(m, np.uint8)
+        rf[:L] = 1
+        horig = original.copy()
+        horig[k - L:] = 0x5A
+        rs16.decode_host(k, m, sb, horig, of, hrec, rf, slice_bytes, engine=eng)
+        assert np.array_equal(horig, original), f"decode, repetition {rep}"
