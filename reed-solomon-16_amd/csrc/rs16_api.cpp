@@ -241,7 +241,7 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
     if ((he = hipMalloc(&e->d_skew_tab, (size_t)GF_ORDER * TAB_DWORDS * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_mul_tab, t.mul_tab.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_log_walsh, GF_ORDER * 2)) != hipSuccess) return fail(he);
-    if ((he = hipMalloc(&e->d_zero_sink, RS16_ZERO_BYTES + RS16_SINK_BYTES)) != hipSuccess) return fail(he);
+    if ((he = hipMalloc(&e->d_zero_sink, RS16_ZERO_BYTES)) != hipSuccess) return fail(he);
     if ((he = hipMemset(e->d_zero_sink, 0, RS16_ZERO_BYTES)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_skew_tab, t.skew_tab.data(), t.skew_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);
     if ((he = hipMemcpy(e->d_mul_tab, t.mul_tab.data(), t.mul_tab.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(he);

@@ -93,7 +93,6 @@ static PassArgs base_args(const rs16_engine* e, size_t S) {
     a.skew_tab = e->d_skew_tab;
     a.mul_tab = e->d_mul_tab;
     a.zero = e->d_zero_sink;
-    a.sink = e->d_zero_sink + RS16_ZERO_BYTES;
     a.S_in = a.S_out = a.S_seg = a.S_rest = S;
     a.qrow = (uint32_t)(S / 8);
     return a;

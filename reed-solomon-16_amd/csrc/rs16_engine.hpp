@@ -77,7 +77,7 @@ struct rs16_engine {
     uint32_t* d_col_img = nullptr;   // column codec table images (HostTables::col_img)
     uint32_t* d_col_v = nullptr;     // column codec eval_poly tables (HostTables::col_v)
     uint16_t* d_log_walsh = nullptr;
-    uint8_t* d_zero_sink = nullptr;  // zero page + store sink (PassArgs::zero / sink)
+    uint8_t* d_zero_sink = nullptr;  // zero page (PassArgs::zero, ColArgs::zero)
     // scratch
     rs16::DevBuf ws_z, ws_u, ws_fd, ws_work32, ws_elog, ws_flags;
     rs16::DevBuf ws_zflag;  // decode: per DEC_FIRST tile, 1 = no received row (tile skipped, rows zero)

@@ -130,14 +130,11 @@ struct PassArgs {
     // Received rows of the decode as a bitmap (bit r & 31 of word r >> 5), so
     // that a tile's flags are two scalar loads (rows of segments A and B).
     const uint32_t* rbits;
-    // Branch-free memory access: a row that is not read (absent / zero /
-    // out-of-slab lanes) is read from `zero` (RS16_ZERO_BYTES of zeros, at
-    // offset offL & 0x7FFF), and in the pipelined build a row that is not
-    // written goes to `sink` (RS16_SINK_BYTES nobody reads), so every load
-    // and store of an item is unconditional and the compiler's vmcnt waits
-    // stay exact across the pipelined items.
+    // Branch-free loads: a row that is not read (absent / zero / out-of-slab
+    // lanes) is read from `zero` (RS16_ZERO_BYTES of zeros, at offset
+    // offL & 0x7FFF), so every load of an item is unconditional and the
+    // compiler's vmcnt waits for the staged tables stay exact.
     const uint8_t* zero;
-    uint8_t* sink;
     // eval_poly with its last 256-point FWHT (row bits 0-7) left undone
     // (launch_eval_poly_from_flags, last_lo = false): DEC_FIRST / DEC_LAST at
     // T = 8 finish it for their tile's rows in LDS.  nullptr: use elog.
@@ -228,7 +225,6 @@ enum DiagFlags : int {
 extern int g_diag;
 
 constexpr size_t RS16_ZERO_BYTES = 65536;
-constexpr size_t RS16_SINK_BYTES = 1 << 20;
 
 // Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.
 hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, hipStream_t s);

@@ -204,17 +204,6 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
     return ur < lim && lr < lim - ur;
 }
 
-// Diagnostic ablation builds (never the shipped library):
-//   -DRS16_ABLATE=1  compile the butterfly layers out (memory + staging only)
-//   -DRS16_ABLATE=2  compile HBM loads/stores out (compute only)
-//   -DRS16_ABLATE=3  as 1, and no table staging
-//   -DRS16_ABLATE=4  as 1, and no LDS exchanges / formal derivative
-//   -DRS16_ABLATE=5  loads / stores kept, but to L2-resident scratch (no HBM)
-//   -DRS16_ABLATE=7  butterflies kept, no LDS layout switches / formal derivative
-#ifndef RS16_ABLATE
-#define RS16_ABLATE 0
-#endif
-
 // Diagnostic timeline build (-DRS16_STAMPS=1, never the shipped library):
 // wave 0 of every workgroup stores s_memtime at phase boundaries to
 // stamps[block * 16 + phase] (phase 15: s_memrealtime at the end, 14 at
@@ -232,7 +221,10 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
 // later schedule 607; none 595 / 594.
 // At point `at` of program P's item (0 staged, 1 first layout-A layers done,
 // 2 first direction done, 3 layout-B FFT done, 4 last switch done, 5 stores).
-template <int P, int at> __device__ __forceinline__ void prio() {
+// (A static pair schedule -- slots 0-1 at priority 3 for the whole item,
+// slots 2-3 at 0 -- measured no better on the T = 7 passes and 3.5 us worse
+// on the T = 8 ones, same-box A/B x 3, round 4.)
+template <int P, int at, int T = 7> __device__ __forceinline__ void prio() {
     constexpr int v[6] = {3, 2, -1, 1, -1, 0};
     if constexpr (v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
 }
@@ -261,14 +253,6 @@ __host__ __device__ constexpr int vmcnt_wait(int n) { return (n & 15) | ((n >> 4
 
 // Row loads / stores at an address that includes the lane's offset.
 __device__ __forceinline__ void ld_ptr(const PassArgs& a, const gbyte* p, bool ok, uint32_t& L, uint32_t& H) {
-#if RS16_ABLATE == 2
-    L = (uint32_t)(uintptr_t)p ^ (ok ? 1u : 0u);
-    H = L * 3u;
-    return;
-#endif
-#if RS16_ABLATE == 5
-    p = (const gbyte*)(a.zero + ((uintptr_t)p & 0x3FFCu));  // L2-resident 16 KiB
-#endif
     (void)a;
     L = H = 0;
     if (ok) {
@@ -281,12 +265,6 @@ __device__ __forceinline__ void ld_ptr(const PassArgs& a, const gbyte* p, bool o
 }
 template <bool NT>
 __device__ __forceinline__ void st_ptr(const PassArgs& a, gbyte* p, bool ok, uint32_t L, uint32_t H) {
-#if RS16_ABLATE == 2
-    if ((L ^ H) != 0x9e3779b9u) return;
-#endif
-#if RS16_ABLATE == 5
-    p = (gbyte*)(a.sink + ((uintptr_t)p & 0x3FFFCu));  // L2-resident 256 KiB
-#endif
     (void)a;
     if (ok) {
         gu32* g = (gu32*)p;
@@ -305,14 +283,10 @@ __device__ __forceinline__ void st_ptr(const PassArgs& a, gbyte* p, bool ok, uin
 // before the rows) count exactly instead of waiting for every row.
 __device__ __forceinline__ void ld_sel(const PassArgs& a, const gbyte* p, bool ok, uint32_t offL, uint32_t& L,
                                        uint32_t& H) {
-#if RS16_ABLATE == 2 || RS16_ABLATE == 5
-    ld_ptr(a, p, ok, L, H);
-#else
     // (offL & 0x7FFF: the zero page is RS16_ZERO_BYTES = 64 KiB, rows can be wider)
     const gu32* g = (const gu32*)(ok ? p : (const gbyte*)a.zero + (offL & 0x7FFFu));
     L = g[0];
     H = g[8];
-#endif
 }
 // Per-lane byte offset of the lane's quad in the row lane_rows below the
 // wave's row: 32 bits (global_load/store with an SGPR base) when the launch
@@ -353,7 +327,6 @@ template <int T, int N> struct Stager {
 
     // table i = entry(i) of `tabs` (TAB_DWORDS dwords per entry)
     template <class F> __device__ __forceinline__ void issue(const uint32_t* tabs, F entry) {
-        if (RS16_ABLATE == 3) return;
         const u32x4* tab = (const u32x4*)tabs;
 #pragma unroll
         for (int i = 0; i < PER; i++) {
@@ -362,7 +335,6 @@ template <int T, int N> struct Stager {
         }
     }
     __device__ __forceinline__ void commit(uint4* dst) const {
-        if (RS16_ABLATE == 3) return;
         u32x4* d = (u32x4*)dst;
 #pragma unroll
         for (int i = 0; i < PER; i++) {
@@ -616,7 +588,7 @@ template <int P, int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int P
 __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                        const PassArgs& a, const uint4* tab1, const uint4* tab2,
                                        uint32_t zmask = 0, const FIN& fin = FIN()) {
-    if constexpr (KB1 > KB0 && (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6 || RS16_ABLATE == 7)) {
+    if constexpr (KB1 > KB0) {
         uint32_t t0[20];
         load_table_lds(t0, group_table<T, LB, KB0, KB1, FFT, 0, IN_TAB2>(c, tab1, tab2));
         GroupLoop<P, T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0, FIN>::run(L, H, c, a, tab1, tab2, t0, zmask, fin);
@@ -721,7 +693,6 @@ template <int T, int NQR, bool FROM_B, class MID = NoMid>
 __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                          uint2* lds, MID mid = MID()) {
     constexpr int QL = Geo<T>::Q / NQR;
-    if (RS16_ABLATE == 4 || RS16_ABLATE == 7) return mid();
 #pragma unroll
     for (int r = 0; r < NQR; r++) {
         if (my_round<NQR>(c, r)) put_rows<T, QL, FROM_B>(L, H, c, lds);
@@ -749,7 +720,6 @@ __device__ __forceinline__ void tile_fd(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
                                         const uint32_t (&SL)[Geo<T>::NR], const uint32_t (&SH)[Geo<T>::NR],
                                         const Thr& c, uint2* lds) {
     constexpr int QL = Geo<T>::Q / NQR;
-    if (RS16_ABLATE == 4 || RS16_ABLATE == 7) return;
     if constexpr (T <= 4) {
         fd_rows<T, QL, LB>(L, H, SL, SH, c, lds);
     } else {
@@ -1031,7 +1001,7 @@ template <int P, int T> struct TileStage {
                     const uint32_t r = row_rel<T>(c, a, k) + a.row_base_in;
                     const bool rcv = (rw[i] >> (r & 31)) & 1u;
                     const uint32_t e = rcv ? log_of(k, r) : ZERO_ENTRY;
-                    if (RS16_ABLATE != 3 && idx < (1u << T) * 5)
+                    if (idx < (1u << T) * 5)
                         se.v[i] = tab[(size_t)e * (TAB_DWORDS / 4) + idx % 5];
                 }
             };
@@ -1130,8 +1100,8 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     constexpr bool ZERO_SKIP = P == DEC_MID && T > 4 && G::R == 4;
     // stores inside the last FFT block (one-item build, 16 rows per lane, not
     // the output-pruned DEC_MID; the reveal stores measured slower inside it)
-    constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && P != DEC_MID && PT::STORE != ST_RESTORE &&
-                           (RS16_ABLATE == 0 || RS16_ABLATE == 2 || RS16_ABLATE == 6 || RS16_ABLATE == 7) && PT::FFT && T > 4;
+    constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && P != DEC_MID && PT::STORE != ST_RESTORE && PT::FFT &&
+                           T > 4;
     uint2* lds = (uint2*)smem;
     const uint4* tab1 = (const uint4*)(smem + SM::TAB1_OFF);
     const uint4* tab2 = (const uint4*)(smem + SM::TAB2_OFF);
@@ -1174,7 +1144,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         if constexpr (ZERO_SKIP) skip_a = __all(d.zrow == (1u << NR) - 1);
         if (!skip_a) layers<P, T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
         stamp(a, 3);
-        prio<P, 1>();
+        prio<P, 1, T>();
         if constexpr (T > 4) {
             Stager<T, (LateS2<P, T>::value ? G::TSPLIT : 0)> s3;
             if constexpr (LateS2<P, T>::value) s3.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
@@ -1187,7 +1157,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             in_b = true;
         }
         stamp(a, 5);
-        prio<P, 2>();
+        prio<P, 2, T>();
     }
     // ---------------- formal derivative (tile bits) ----------------
     if constexpr (PT::FD) {
@@ -1201,7 +1171,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             layers<P, T, true, R, (T > 4 ? T : R), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
             stamp(a, 7);
-            prio<P, 3>();
+            prio<P, 3, T>();
             // reveal multipliers: requested before the last layout switch,
             // written to LDS between its barriers (read after the layers)
             RevealStage<P, (LateReveal<P, T>::value ? T : 0)> rs;
@@ -1217,7 +1187,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                 if constexpr (LateReveal<P, T>::value) rs.commit(a, c, smem);
             });
             stamp(a, 8);
-            prio<P, 4>();
+            prio<P, 4, T>();
             in_b = false;
         }
         bool need = true;
@@ -1242,7 +1212,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         return;
     }
 
-    prio<P, 5>();
+    prio<P, 5, T>();
     // ---------------- store ----------------
     // The next item's loads were issued before this item's butterflies and
     // have landed by now: retire them before the stores, so that the stores
@@ -1349,7 +1319,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
         }
     }
     stamp(a, 1);
-    prio<P, 0>();
+    prio<P, 0, T>();
     st.template finish<EARLY>(a, c, smem);
     stamp(a, 2);
     process_item<P, T>(a, c, tile, slab, cur, smem);
