@@ -256,6 +256,25 @@ int rs16_decode_device_batch(rs16_engine* eng, size_t original_count, size_t rec
                              const uint8_t* d_original_received, const void* d_recovery, size_t recovery_stride,
                              const uint8_t* d_recovery_received, size_t original_received_count,
                              size_t recovery_received_count, void* stream, rs16_error* err);
+/* rs16_decode_device for `nstripes` independent stripes, EACH WITH ITS OWN
+ * received set (the reference decodes one stripe per call with that call's
+ * received shards: src/lib.rs:287-344, src/rate/decoder_work.rs:62-139):
+ * stripe i's flags at d_original_received + i * original_received_stride and
+ * d_recovery_received + i * recovery_received_stride (strides >= the counts),
+ * its received counts in the HOST arrays original_received_counts[i] /
+ * recovery_received_counts[i] (which must equal its flags, as for
+ * rs16_decode_device), its shards as for rs16_decode_device_batch.  Errors are
+ * the per-stripe ones (NotEnoughShards with the first failing stripe's
+ * numbers).  One eval_poly launch with a grid row per stripe, then pass
+ * launches shared by all stripes.  Every stripe's result equals
+ * rs16_decode_device on it alone.  (rs16_decode_check does not cover it.) */
+int rs16_decode_device_batch_varied(rs16_engine* eng, size_t original_count, size_t recovery_count,
+                                    size_t shard_bytes, size_t nstripes, void* d_original, size_t original_stride,
+                                    const uint8_t* d_original_received, size_t original_received_stride,
+                                    const void* d_recovery, size_t recovery_stride,
+                                    const uint8_t* d_recovery_received, size_t recovery_received_stride,
+                                    const size_t* original_received_counts, const size_t* recovery_received_counts,
+                                    void* stream, rs16_error* err);
 /* Checked mode of the engine's last decode: waits for `stream` and compares
  * the received counts that decode was given with the rows the device flags
  * mark received (the eval_poly kernels count them per 64-row chunk as they

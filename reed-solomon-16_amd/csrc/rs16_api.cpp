@@ -1295,6 +1295,72 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
     return set_error(err, RS16_OK);
 }
 
+// rs16_decode_device for `nstripes` independent stripes, each with its own
+// received set (reed_solomon_16::decode, src/lib.rs:287-344, once per stripe;
+// src/rate/decoder_work.rs:62-139 counts every call's own received shards):
+// stripe i's flags at d_*_received + i * *_received_stride bytes, its counts
+// in the host arrays.  One launch of the eval kernels with a grid row per
+// stripe (per-stripe erasure logs, received bitmaps, zero tiles, lost
+// ranges), then the pass launches shared by all stripes, each workgroup
+// reading its stripe's metadata.  Path: the half-transform decode when no
+// stripe received an original, else the general decode for all; the
+// first-pass tiles launched are the union over the stripes.
+extern "C" int rs16_decode_device_batch_varied(rs16_engine* e, size_t k, size_t m, size_t S, size_t nstripes,
+                                               void* d_original, size_t original_stride,
+                                               const uint8_t* d_original_received, size_t original_received_stride,
+                                               const void* d_recovery, size_t recovery_stride,
+                                               const uint8_t* d_recovery_received, size_t recovery_received_stride,
+                                               const size_t* original_received_counts,
+                                               const size_t* recovery_received_counts, void* stream, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    e->forget_decode();
+    if (nstripes == 0) return set_error(err, RS16_OK);
+    if (!d_original || !d_recovery || !d_original_received || !d_recovery_received || !original_received_counts ||
+        !recovery_received_counts || original_stride < k * S || recovery_stride < m * S || original_stride % 64 ||
+        recovery_stride % 64 || original_received_stride < k || recovery_received_stride < m ||
+        nstripes > ((size_t)1 << 16))
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    size_t max_o = 0, max_r = 0;
+    bool any_lost = false;
+    for (size_t i = 0; i < nstripes; i++) {
+        const size_t o = original_received_counts[i], r = recovery_received_counts[i];
+        if (o > k || r > m) return set_error(err, RS16_INVALID_ARGUMENT);
+        if (o + r < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, o, r);  // (the first such stripe)
+        max_o = std::max(max_o, o);
+        max_r = std::max(max_r, r);
+        any_lost |= o < k;
+    }
+    if (!any_lost) return set_error(err, RS16_OK);  // nothing to restore in any stripe
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
+    DecodeGeom g = decode_geom(high, k, m);
+    // (a segment counts as received when any stripe received a shard of it)
+    g.a_recv = high ? max_r : max_o;
+    g.b_recv = high ? max_o : max_r;
+    RS16_HIP(e->ws_z.reserve(nstripes * g.n * S));
+    RS16_HIP(e->ws_u.reserve(nstripes * g.n * S));
+    const uint8_t* orig = (const uint8_t*)d_original;
+    const uint8_t* rec = (const uint8_t*)d_recovery;
+    const uint8_t* seg_a = high ? rec : orig;
+    const uint8_t* seg_b = high ? orig : rec;
+    const size_t bs_a = high ? recovery_stride : original_stride, bs_b = high ? original_stride : recovery_stride;
+    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
+    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
+    const size_t fs_a = high ? recovery_received_stride : original_received_stride;
+    const size_t fs_b = high ? original_received_stride : recovery_received_stride;
+    const uint32_t vary = nstripes > 1 ? (uint32_t)nstripes : 0;
+    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, S, nstripes, vary, fs_a, fs_b)) return rc;
+    if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
+                                  (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, s, err, nstripes, bs_a, bs_b,
+                                  original_stride))
+        return rc;
+    e->forget_decode();
+    if (int rc = e->scratch_done(s, err)) return rc;
+    return set_error(err, RS16_OK);
+}
+
 // ---------------------------------------------------------------------------
 // Device memory helpers.
 // ---------------------------------------------------------------------------

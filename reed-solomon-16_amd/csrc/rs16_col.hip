@@ -485,6 +485,10 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     const uint32_t offL = (q >> 3) * 64u + (q & 7u) * 4u;
     const uint8_t* in = a.in + st * a.bs_in + offL;
     uint8_t* out = a.out + st * a.bs_out + offL;
+    // stripes with losses of their own (all strides 0 when shared)
+    if (a.flags) a.flags += st * a.bs_flags;
+    if (a.flags_o) a.flags_o += st * a.bs_flags_o;
+    if (a.elog) a.elog += st * a.bs_elog;
 
     // ---- requests: the rows, the tables (LDS-DMA), the decoder's erasure data
     // (the compiler drains every LDS-DMA load at the first use of an ordinary

@@ -405,14 +405,18 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, size_t S_user, cons
 
 // Erasure logs e = eval_poly(erasure vector) into ws_elog (2-3 small kernels).
 int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
-                             rs16_error* err, size_t S, size_t nstripes) {
-    RS16_HIP(ws_work32.reserve(GF_ORDER * 4));
-    RS16_HIP(ws_elog.reserve(GF_ORDER * 4));
-    RS16_HIP(ws_zflag.reserve(256));
-    RS16_HIP(ws_rbits.reserve(GF_ORDER / 8));
-    RS16_HIP(ws_lost.reserve(256 * 8 + 16));
+                             rs16_error* err, size_t S, size_t nstripes, uint32_t vary, size_t bs_fa, size_t bs_fb) {
+    const size_t nv = vary > 1 ? vary : 1;
+    RS16_HIP(ws_work32.reserve(nv * VARY_WORK * 4));
+    RS16_HIP(ws_elog.reserve(nv * VARY_WORK * 4));
+    RS16_HIP(ws_zflag.reserve(nv * VARY_ZFLAGS));
+    RS16_HIP(ws_rbits.reserve(nv * VARY_RBITS * 4));
+    RS16_HIP(ws_lost.reserve(nv * VARY_LOST * 4));
     RS16_HIP(ws_rcount.reserve(GF_ORDER / 64 * 8));
-    ErasureSpec es;
+    var_ns = vary > 1 ? vary : 0;
+    var_bs_fa = vary > 1 ? bs_fa : 0;
+    var_bs_fb = vary > 1 ? bs_fb : 0;
+    ErasureSpec es{};
     es.flags_a = flags_a;
     es.flags_b = flags_b;
     es.a_count = g.a_count;
@@ -436,6 +440,19 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.rcount = (uint32_t*)ws_rcount.p;
     last_dec = g;
     last_dec_valid = true;
+    if (var_ns) {
+        // every stripe's own metadata; no received counts (rs16_decode_check
+        // covers the single-pattern calls)
+        es.nstripes = var_ns;
+        es.bs_fa = var_bs_fa;
+        es.bs_fb = var_bs_fb;
+        es.bs_work = es.bs_elog = VARY_WORK;
+        es.bs_rbits = VARY_RBITS;
+        es.bs_zflags = VARY_ZFLAGS;
+        es.bs_lost = VARY_LOST;
+        es.rcount = nullptr;
+        last_dec_valid = false;
+    }
     // High-rate half decodes of 2^9 / 2^10-row halves through the column
     // codec: it evaluates the polynomial itself (an n-point XOR convolution,
     // rs16_col.hip) and writes rcount; no kernel here.
@@ -501,6 +518,15 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.rest_seg_b = g.high ? 1 : 0;
     a.rbits = (const uint32_t*)ws_rbits.p;
     a.skew_ifft = a.skew_fft = 0;
+    if (var_ns) {  // stripes with losses of their own (decode_eval's per-stripe metadata)
+        a.bs_fa = var_bs_fa;
+        a.bs_fb = var_bs_fb;
+        a.bs_elog = VARY_WORK;
+        a.bs_rbits = VARY_RBITS;
+        a.bs_zflags = VARY_ZFLAGS;
+        a.bs_lost = VARY_LOST;
+        rcount = nullptr;
+    }
     // nst > 1: independent stripes with one erasure pattern (rs16_decode_device_batch):
     // every launch covers all of them (PassArgs::stripe_tiles); stripe i's
     // segments / restored originals at + i bs_a / bs_b / bs_rest, its work
@@ -549,6 +575,9 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
             c.base_out = c.skew_fft = dst;
             c.chunk = g.chunk;
             c.e_pad = 1;  // (high rate: padding rows erased, nothing above the originals)
+            c.bs_flags = g.high ? var_bs_fa : var_bs_fb;
+            c.bs_flags_o = var_bs_fb;
+            c.bs_elog = var_ns ? VARY_WORK : 0;
             if (col_eval) {
                 // eval_poly in the kernel (decode_eval launched nothing)
                 c.flags_o = flags_b;
@@ -598,6 +627,8 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         c.bs_out = bs_rest;
         c.out_rows = g.high ? g.b_count : g.a_count;
         c.rcount = rcount;
+        c.bs_flags = var_bs_fa;
+        c.bs_flags_o = var_bs_fb;
         return col(c, L, COL_DEC_GEN, s, err);
     }
     if (L <= 8) {

@@ -194,8 +194,18 @@ struct rs16_engine {
     // S / nstripes: the width of the decode_passes launches that follow (0:
     // unknown); when the column codec will run them as a high-rate half
     // decode it computes eval_poly itself and no kernel is launched here.
+    // vary > 1: nstripes = vary stripes with losses of their own, stripe i's
+    // flags at flags_a / flags_b + i bs_fa / bs_fb bytes: one grid row of the
+    // eval kernels per stripe, per-stripe metadata (VARY_* strides below),
+    // which the decode_passes that follow read (var_* state).
     int decode_eval(const rs16::DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
-                    rs16_error* err, size_t S = 0, size_t nstripes = 1);
+                    rs16_error* err, size_t S = 0, size_t nstripes = 1, uint32_t vary = 0, size_t bs_fa = 0,
+                    size_t bs_fb = 0);
+    // per-stripe decode metadata of a batch with losses of its own
+    static constexpr uint32_t VARY_WORK = rs16::GF_ORDER, VARY_RBITS = rs16::GF_ORDER / 32, VARY_ZFLAGS = 256,
+                              VARY_LOST = 520;
+    uint32_t var_ns = 0;           // last decode_eval: stripes with losses of their own (0: shared)
+    uint64_t var_bs_fa = 0, var_bs_fb = 0;
     // rcount: where a column decode that evaluates the polynomial itself
     // writes the received counts (ErasureSpec::rcount layout): ws_rcount on
     // the call's own stream, a buffer of their own for concurrent slots.

@@ -160,6 +160,13 @@ struct PassArgs {
     // encoder's FFTs of every recovery chunk read the one transformed chunk
     // of originals instead of copies of it.
     uint32_t in_rows_mask;
+    // Batched stripes with losses of their own (rs16_decode_device_batch_varied):
+    // stripe s also reads flags_a / flags_b displaced by s bs_fa / bs_fb
+    // bytes and its own decode metadata -- elog / ework + s bs_elog words,
+    // rbits + s bs_rbits words, zflags + s bs_zflags bytes, lostrange + s
+    // bs_lost words (ErasureSpec's per-stripe outputs).  All 0: shared.
+    uint64_t bs_fa, bs_fb;
+    uint32_t bs_elog, bs_rbits, bs_zflags, bs_lost;
 };
 
 // One-launch codec for 2^9 / 2^10-row transforms (rs16_col.hip): one
@@ -204,6 +211,10 @@ struct ColArgs {
     uint32_t skew_ifft, skew_fft;
     uint32_t base_in, base_out;
     uint64_t bs_in, bs_out;
+    // stripes with losses of their own: flags / flags_o + st bs_flags /
+    // bs_flags_o bytes, elog + st bs_elog words (0: shared by all stripes)
+    uint64_t bs_flags, bs_flags_o;
+    uint32_t bs_elog;
     uint64_t* stamps;           // RS16_STAMPS builds: phase timeline (rs16_engine_set_stamps)
 };
 int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec covers
@@ -263,6 +274,15 @@ struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.r
     // (rs16_decode_check compares their sums with the caller's counts).
     uint32_t* rcount;
     uint64_t* stamps;          // RS16_STAMPS builds: eval timeline (rs16_engine_set_stamps)
+    // Stripes with losses of their own (rs16_decode_device_batch_varied):
+    // nstripes > 1 evaluates stripe y in grid row y, with its flags at
+    // flags_a / flags_b + y bs_fa / bs_fb bytes and its outputs displaced by
+    // y times bs_work (work / out words), bs_elog (last_lo output words),
+    // bs_rbits (words), bs_zflags (bytes), bs_lost (lostpart / lostrange
+    // words).  rcount must be nullptr then.  0 / 1: one stripe.
+    uint32_t nstripes;
+    uint64_t bs_fa, bs_fb;
+    uint32_t bs_work, bs_elog, bs_rbits, bs_zflags, bs_lost;
 };
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo);

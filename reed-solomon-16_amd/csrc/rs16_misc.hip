@@ -136,6 +136,18 @@ __device__ __forceinline__ void fwht256_lds(uint32_t* s) {
     __syncthreads();
 }
 
+// Stripe y = blockIdx.y of a batch with losses of its own (ErasureSpec::nstripes):
+// its flags and its outputs.
+__device__ __forceinline__ void stripe_spec(ErasureSpec& e) {
+    const uint32_t y = blockIdx.y;
+    if (y == 0) return;
+    if (e.flags_a) e.flags_a += y * e.bs_fa;
+    if (e.flags_b) e.flags_b += y * e.bs_fb;
+    if (e.rbits) e.rbits += y * e.bs_rbits;
+    if (e.zflags) e.zflags += y * e.bs_zflags;
+    if (e.lostpart) e.lostpart += y * e.bs_lost;
+    if (e.lostrange) e.lostrange += y * e.bs_lost;
+}
 __device__ __forceinline__ uint32_t erasure_at(const ErasureSpec& e, uint32_t i) {
     if (i < e.a_count) return e.flags_a ? (((cu8p)e.flags_a)[i] ? 0u : 1u) : 0u;
     if (i < e.chunk) return e.pad_fill;
@@ -234,11 +246,16 @@ __global__ void __launch_bounds__(256) fwht_hi_kernel(ErasureSpec e, const uint3
 
 // Contiguous 256-point FWHT; if MULW, then multiply by log_walsh mod 65535 and
 // do the contiguous FWHT again (the middle of eval_poly).
+// (grid row y: in32 / out32 displaced by y bs_in / bs_out words -- the
+// stripes of a batch with losses of their own)
 template <bool MULW, int IN16, int OUT16>
 __global__ void __launch_bounds__(256) fwht_lo_kernel(const uint32_t* in32, const uint16_t* in16, uint32_t* out32,
-                                                       uint16_t* out16, const uint16_t* log_walsh) {
+                                                       uint16_t* out16, const uint16_t* log_walsh, uint32_t bs_in = 0,
+                                                       uint32_t bs_out = 0) {
     __shared__ uint32_t s[256];
     const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+    if (in32) in32 += blockIdx.y * bs_in;
+    if (out32) out32 += blockIdx.y * bs_out;
     s[threadIdx.x] = IN16 ? in16[idx] : in32[idx];
     fwht256_lds(s);
     if (MULW) {
@@ -254,6 +271,8 @@ __global__ void __launch_bounds__(256) fwht_lo_kernel(const uint32_t* in32, cons
 // received bitmap (ballots) and zero-tile flags.
 __global__ void __launch_bounds__(64) fwht_lo_flags_kernel(ErasureSpec e, uint32_t* out32) {
     const uint32_t base = blockIdx.x * 256u, lane = threadIdx.x;
+    stripe_spec(e);
+    out32 += blockIdx.y * e.bs_work;
     uint32_t v[4];
     uint64_t rmask[4], lmask[4];
 #pragma unroll
@@ -276,6 +295,9 @@ __global__ void __launch_bounds__(64) fwht_lo_flags_kernel(ErasureSpec e, uint32
 __global__ void __launch_bounds__(64) fwht_hi_mulw_kernel(ErasureSpec e, const uint32_t* in32, uint32_t* out32,
                                                           const uint16_t* log_walsh) {
     const uint32_t lane = threadIdx.x;
+    stripe_spec(e);
+    in32 += blockIdx.y * e.bs_work;
+    out32 += blockIdx.y * e.bs_work;
     uint32_t v[4], lw[4];
     // LogWalsh does not depend on the previous kernel: its loads go first
 #pragma unroll
@@ -325,10 +347,6 @@ __device__ __forceinline__ int block_region(const ErasureSpec& e, uint32_t base)
     if (base - e.chunk < e.b_count) return 2;
     return 3;
 }
-// (RS16_EVAL_ABL, timing-only builds: 3 = an empty kernel)
-#ifndef RS16_EVAL_ABL
-#define RS16_EVAL_ABL 0
-#endif
 #ifndef RS16_STAMPS
 #define RS16_STAMPS 0
 #endif
@@ -354,6 +372,8 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
     __shared__ int xs[256];
     __shared__ uint32_t lr[2][4];
     const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    stripe_spec(e);
+    out32 += blockIdx.y * e.bs_work;
     estamp(e, 0);
     uint32_t lw[4];
     if (wv == 0) {
@@ -489,15 +509,16 @@ static bool eval_fused_ok(const ErasureSpec& e) {
 
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
-    if (!(g_diag & DIAG_EVAL_TWO_KERNEL) && eval_fused_ok(e)) {
-        hipLaunchKernelGGL(eval_fused_kernel, dim3(256), dim3(256), 0, s, e, work, log_walsh);
+    const uint32_t ns = e.nstripes > 1 ? e.nstripes : 1;
+    if (!(g_diag & DIAG_EVAL_TWO_KERNEL) && eval_fused_ok(e) && (ns == 1 || (e.bs_fa % 16 == 0 && e.bs_fb % 16 == 0))) {
+        hipLaunchKernelGGL(eval_fused_kernel, dim3(256, ns), dim3(256), 0, s, e, work, log_walsh);
     } else {
-        hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256), dim3(64), 0, s, e, work);
-        hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256), dim3(64), 0, s, e, work, work, log_walsh);
+        hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256, ns), dim3(64), 0, s, e, work);
+        hipLaunchKernelGGL(fwht_hi_mulw_kernel, dim3(256, ns), dim3(64), 0, s, e, work, work, log_walsh);
     }
     if (last_lo)
-        hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(256), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
-                           nullptr);
+        hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(256, ns), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
+                           nullptr, e.bs_work, e.bs_elog);
     return hipGetLastError();
 }
 // eval_poly of a high-rate decode with n <= 2048 work rows:
@@ -531,7 +552,8 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
     __shared__ int part[2][4][NB];  // per-wave parts of x and z
     __shared__ uint32_t words[8];   // block j's received bitmap (zero-tile flags)
     const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (RS16_EVAL_ABL == 3) return;
+    stripe_spec(e);
+    z += blockIdx.y * e.bs_work;
     estamp(e, 0);
     const uint32_t lw = log_walsh[t * 256u + j];  // in flight from the start
     // flag bytes of rows 256 h' + t, all loads issued before the first use
@@ -629,16 +651,17 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
 hipError_t launch_eval_poly_small(const ErasureSpec& e, uint32_t n, uint32_t* work, uint32_t* out_elog,
                                   const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
     const uint32_t nb = n <= 256 ? 1 : n / 256;
+    const uint32_t ns = e.nstripes > 1 ? e.nstripes : 1;
     switch (nb) {
-        case 1: hipLaunchKernelGGL(eval_small_kernel<1>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
-        case 2: hipLaunchKernelGGL(eval_small_kernel<2>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
-        case 4: hipLaunchKernelGGL(eval_small_kernel<4>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
-        case 8: hipLaunchKernelGGL(eval_small_kernel<8>, dim3(256), dim3(256), 0, s, e, log_walsh, work); break;
+        case 1: hipLaunchKernelGGL(eval_small_kernel<1>, dim3(256, ns), dim3(256), 0, s, e, log_walsh, work); break;
+        case 2: hipLaunchKernelGGL(eval_small_kernel<2>, dim3(256, ns), dim3(256), 0, s, e, log_walsh, work); break;
+        case 4: hipLaunchKernelGGL(eval_small_kernel<4>, dim3(256, ns), dim3(256), 0, s, e, log_walsh, work); break;
+        case 8: hipLaunchKernelGGL(eval_small_kernel<8>, dim3(256, ns), dim3(256), 0, s, e, log_walsh, work); break;
         default: return hipErrorInvalidValue;
     }
     if (last_lo)
-        hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(nb), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
-                           nullptr);
+        hipLaunchKernelGGL((fwht_lo_kernel<false, 0, 0>), dim3(nb, ns), dim3(256), 0, s, work, nullptr, out_elog, nullptr,
+                           nullptr, e.bs_work, e.bs_elog);
     return hipGetLastError();
 }
 // Engine-level fwht / eval_poly (the C ABI ops): the layers run in the

@@ -1265,6 +1265,15 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
         a.seg_a += st * a.bs_seg;
         a.seg_b += st * a.bs_seg_b;
         a.rest += st * a.bs_rest;
+        // stripes with losses of their own: their flags and decode metadata
+        // (all strides 0 when the stripes share one erasure pattern)
+        if (a.flags_a) a.flags_a += st * a.bs_fa;
+        if (a.flags_b) a.flags_b += st * a.bs_fb;
+        if (a.elog) a.elog += st * a.bs_elog;
+        if (a.ework) a.ework += st * a.bs_elog;
+        if (a.rbits) a.rbits += st * a.bs_rbits;
+        if (a.zflags) a.zflags += st * a.bs_zflags;
+        if (a.lostrange) a.lostrange += st * a.bs_lost;
     }
     tile += a.tile_base;
     c.b_low = tile & ((1u << a.lo) - 1);

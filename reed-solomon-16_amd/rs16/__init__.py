@@ -634,6 +634,23 @@ def decode_device_batch(original_count, recovery_count, shard_bytes, nstripes, d
                                           original_received_count, recovery_received_count, stream, C.byref(err)), err)
 
 
+def decode_device_batch_varied(original_count, recovery_count, shard_bytes, nstripes, d_original, original_stride,
+                               d_original_received, original_received_stride, d_recovery, recovery_stride,
+                               d_recovery_received, recovery_received_stride, original_received_counts,
+                               recovery_received_counts, stream=None, engine: Optional[Engine] = None):
+    """rs16_decode_device_batch_varied: nstripes stripes, each with its own
+    received flags (stripe i's at d_*_received + i * *_received_stride) and
+    counts (host sequences of nstripes ints)."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    oc = (C.c_size_t * nstripes)(*[int(x) for x in original_received_counts])
+    rc = (C.c_size_t * nstripes)(*[int(x) for x in recovery_received_counts])
+    _check(lib().rs16_decode_device_batch_varied(
+        eng.h, original_count, recovery_count, shard_bytes, nstripes, Engine._ptr(d_original), original_stride,
+        Engine._ptr(d_original_received), original_received_stride, Engine._ptr(d_recovery), recovery_stride,
+        Engine._ptr(d_recovery_received), recovery_received_stride, oc, rc, stream, C.byref(err)), err)
+
+
 def decode_device(original_count, recovery_count, shard_bytes, d_original, d_original_received, d_recovery,
                   d_recovery_received, original_received_count, recovery_received_count, stream=None,
                   engine: Optional[Engine] = None, check: bool = False):

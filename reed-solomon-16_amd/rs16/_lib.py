@@ -81,6 +81,8 @@ SIGNATURES = {
     "rs16_encode_device": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _e]),
     "rs16_encode_device_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _sz, _p, _e]),
     "rs16_decode_device_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _p, _sz, _p, _sz, _sz, _p, _e]),
+    "rs16_decode_device_batch_varied": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _sz, _p, _sz, _p, _sz, _p, _p, _p,
+                                             _e]),
     "rs16_decode_device": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _p, _sz, _sz, _p, _e]),
     "rs16_decode_check": (_i, [_p, _p, _e]),
     "rs16_device_alloc": (_p, [_p, _sz, _e]),
