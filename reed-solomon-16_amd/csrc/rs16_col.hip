@@ -68,30 +68,30 @@ template <int B0, int B1> __device__ __forceinline__ uint32_t brow(uint32_t t, i
     return lo | (mid << (B0 + 1)) | (hi << (B1 + 1)) | ((uint32_t)(m & 1) << B0) | ((uint32_t)(m >> 1) << B1);
 }
 
-// LDS layout (bytes), 2 (2^L - 1) x 80 = 160 KiB at L = 10:
-//   A [0, (N-1) 80)            the IFFT's tables in tile-group order (layer kb
-//                              at group N - 2^(L-kb), group j = row >> (kb+1))
-//   B [A end, + (N/2-1) 80)    the FFT's tables of groups >= N/2 (layers >= 1)
-//   C [B end, + N/2 80)        the FFT's layer-0 tables
-// The row image of the LDS exchanges (N x 8 bytes) lies over the IFFT's
-// layer-0 tables (dead after the first block); the decoder's erasure logs
-// (2N x 4 bytes) over C, before C's tables are loaded.
+// LDS layout (bytes).  The tables of layers 0 and 1 (3/4 of each
+// direction's 2^L - 1) are each used by one thread in one block (the first
+// IFFT block, the last FFT block): every thread loads its own straight from
+// the image into registers at the start (load_tabs01_img), so LDS holds
+// layers 2 .. L-1 of both directions only, staged by LDS-DMA (2 (N/4 - 1)
+// x 80 bytes, 40 KiB at L = 10), the row image and the erasure logs:
+//   A   the IFFT's tables of groups >= G2 (layer kb at group N - 2^(L-kb),
+//       group j = row >> (kb+1); G2 = 3N/4 = the first group of layer 2)
+//   B   the FFT's, likewise
+//   IMG the row image of the LDS exchanges (N x 8 bytes)
+//   ELOG the decoder's erasure logs / polynomial scratch (2N x 4 bytes)
 template <int L> struct ColSmem {
     static constexpr int N = 1 << L;
+    static constexpr int G0 = N - N / 4;  // first group of layer 2
     static constexpr int A = 0;
-    static constexpr int B = A + (N - 1) * 80;
-    static constexpr int C = B + (N / 2 - 1) * 80;
-    static constexpr int BYTES = C + (N / 2) * 80;
-    static constexpr int IMG = A;
-    static constexpr int ELOG = C;
-    static_assert(N * 8 <= (N / 2) * 80 && 2 * N * 4 <= (N / 2) * 80, "image / logs fit their regions");
+    static constexpr int B = A + (N - 1 - G0) * 80;
+    static constexpr int IMG = B + (N - 1 - G0) * 80;
+    static constexpr int ELOG = IMG + N * 8;
+    static constexpr int BYTES = ELOG + 2 * N * 4;
     static_assert(L >= (int)COL_LMIN && L <= (int)COL_LMAX, "the column codec covers 2^6 .. 2^10 rows");
 };
 
-// The general decoder's 2^11-row transform (COL_DEC_GEN only): the tables
-// of layers 0 and 1 are each used by one thread once, so they are read from
-// the image in HBM / L2 at their block; LDS holds layers 2..10 of both
-// directions, the row image and the erasure logs side by side.
+// The general decoder's 2^11-row transform (COL_DEC_GEN only): the same
+// layout (its logs: N x 4 bytes).
 template <> struct ColSmem<11> {
     static constexpr int N = 2048;
     static constexpr int G0 = N - N / 4;  // first group of layer 2
@@ -99,7 +99,6 @@ template <> struct ColSmem<11> {
     static constexpr int B = A + (N - 1 - G0) * 80;
     static constexpr int IMG = B + (N - 1 - G0) * 80;
     static constexpr int ELOG = IMG + N * 8;
-    static constexpr int C = -1;  // (unused)
     static constexpr int BYTES = ELOG + N * 4;
 };
 
@@ -130,10 +129,8 @@ __device__ __forceinline__ void glb_table(uint32_t (&t)[20], const uint32_t* tab
 template <int L, bool FFT> __device__ __forceinline__ uint32_t tab_off(int kb, uint32_t r) {
     constexpr int N = 1 << L;
     const uint32_t t = (uint32_t)(N - (N >> kb)) + (r >> (kb + 1));
-    if constexpr (L == 11) return (FFT ? ColSmem<11>::B : ColSmem<11>::A) + (t - ColSmem<11>::G0) * 80u;
-    if (!FFT) return ColSmem<L>::A + t * 80u;
-    if (kb == 0) return ColSmem<L>::C + t * 80u;
-    return ColSmem<L>::B + (t - N / 2) * 80u;
+    // (layers >= 2 only: layers 0 and 1 come from registers, load_tabs01_img)
+    return (FFT ? ColSmem<L>::B : ColSmem<L>::A) + (t - ColSmem<L>::G0) * 80u;
 }
 
 // LDS-DMA copy of `bytes` (a multiple of 16) from src to the LDS at dst by
@@ -201,7 +198,7 @@ __device__ __forceinline__ void load_tabs(BlockTabs& w, uint32_t t, const uint8_
     }
     if (D1) lds_table(w.w1, smem, tab_off<L, FFT>(B1, r0));
 }
-// The (0, 1) block's tables at L = 11, from the image (table g at g x 80 bytes).
+// The (0, 1) block's tables, from the image (table g at g x 80 bytes).
 __device__ __forceinline__ void img_table(uint32_t (&t)[20], const uint8_t* img, uint32_t g) {
     const u32x4* p = (const u32x4*)(img + (size_t)g * 80);
 #pragma unroll
@@ -213,8 +210,8 @@ __device__ __forceinline__ void img_table(uint32_t (&t)[20], const uint8_t* img,
         t[4 * i + 3] = v.w;
     }
 }
-__device__ __forceinline__ void load_tabs01_img(BlockTabs& w, uint32_t t, const uint8_t* img) {
-    constexpr uint32_t N = 2048;
+template <int L> __device__ __forceinline__ void load_tabs01_img(BlockTabs& w, uint32_t t, const uint8_t* img) {
+    constexpr uint32_t N = 1u << L;
     const uint32_t r0 = brow<0, 1>(t, 0), r2 = brow<0, 1>(t, 2);
     img_table(w.w0, img, r0 >> 1);
     img_table(w.w2, img, r2 >> 1);
@@ -389,49 +386,63 @@ template <int NT, int PTS> __device__ __forceinline__ void fwht_points(int (&x)[
 // (erased), segment B = originals [chunk, chunk + o_rows) (flags_o), zero
 // above (rate_high.rs:183-197).  PTS = 8: the half decode's 2N work rows;
 // PTS = 4: the general decode's N.
-template <int L, int PTS> __device__ __forceinline__ void col_eval(const ColArgs& a, uint32_t* elds) {
-    constexpr int N = 1 << L, NT = N / 4;
-    const uint32_t t = threadIdx.x, lane = t & 63;
+// In two steps: load() issues every load (the flag bytes and V of the
+// thread's points) -- the kernel calls it before its row loads and table
+// DMA, so that waiting for them does not wait for the DMA (vmcnt counts in
+// issue order) -- and run() computes.
+template <int L, int PTS> struct ColEval {
+    static constexpr int N = 1 << L, NT = N / 4;
     uint8_t f[PTS];
     uint32_t vt[PTS];
+    __device__ __forceinline__ void load(const ColArgs& a) {
+        const uint32_t t = threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < PTS; j++) {
-        const uint32_t p = t + NT * j;
-        const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
-        const uint8_t* fp = in_a && a.flags ? a.flags + p : (in_b && a.flags_o ? a.flags_o + (p - a.chunk) : a.zero);
-        f[j] = *(const __attribute__((address_space(1))) uint8_t*)fp;
-        vt[j] = a.vtab[p];
+        for (int j = 0; j < PTS; j++) {
+            const uint32_t p = t + NT * j;
+            const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
+            const uint8_t* fp = in_a && a.flags ? a.flags + p : (in_b && a.flags_o ? a.flags_o + (p - a.chunk) : a.zero);
+            f[j] = *(const __attribute__((address_space(1))) uint8_t*)fp;
+            vt[j] = a.vtab[p];
+        }
     }
+    // the erasure vector of the thread's points (and the received counts):
+    // the first use of the loaded bytes
     int x[PTS];
-    uint32_t ca = 0, cb = 0;
+    __device__ __forceinline__ void prep(const ColArgs& a) {
+        const uint32_t t = threadIdx.x, lane = t & 63;
+        uint32_t ca = 0, cb = 0;
 #pragma unroll
-    for (int j = 0; j < PTS; j++) {
-        const uint32_t p = t + NT * j;
-        const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
-        const bool rcv = in_a ? (!a.flags || f[j]) : (in_b && (!a.flags_o || f[j]));
-        x[j] = (in_a || in_b) ? !rcv : (int)(p < a.chunk ? a.e_pad : a.e_tail);
-        if (blockIdx.x == 0 && a.rcount) {
-            // (below 64 threads a 64-row chunk spans 64 / NT values of j)
-            constexpr int PER = NT >= 64 ? 1 : 64 / NT;
-            ca += (uint32_t)__popcll(__ballot(rcv && in_a));
-            cb += (uint32_t)__popcll(__ballot(rcv && in_b));
-            if ((j + 1) % PER == 0) {
-                if (lane == 0) {
-                    a.rcount[2 * (p >> 6)] = ca;
-                    a.rcount[2 * (p >> 6) + 1] = cb;
+        for (int j = 0; j < PTS; j++) {
+            const uint32_t p = t + NT * j;
+            const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
+            const bool rcv = in_a ? (!a.flags || f[j]) : (in_b && (!a.flags_o || f[j]));
+            x[j] = (in_a || in_b) ? !rcv : (int)(p < a.chunk ? a.e_pad : a.e_tail);
+            if (blockIdx.x == 0 && a.rcount) {
+                // (below 64 threads a 64-row chunk spans 64 / NT values of j)
+                constexpr int PER = NT >= 64 ? 1 : 64 / NT;
+                ca += (uint32_t)__popcll(__ballot(rcv && in_a));
+                cb += (uint32_t)__popcll(__ballot(rcv && in_b));
+                if ((j + 1) % PER == 0) {
+                    if (lane == 0) {
+                        a.rcount[2 * (p >> 6)] = ca;
+                        a.rcount[2 * (p >> 6) + 1] = cb;
+                    }
+                    ca = cb = 0;
                 }
-                ca = cb = 0;
             }
         }
     }
-    int* sx = (int*)elds;
-    fwht_points<NT, PTS>(x, sx);
+    __device__ __forceinline__ void run(const ColArgs& a, uint32_t* elds) {
+        const uint32_t t = threadIdx.x;
+        int* sx = (int*)elds;
+        fwht_points<NT, PTS>(x, sx);
 #pragma unroll
-    for (int j = 0; j < PTS; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
-    fwht_points<NT, PTS>(x, sx);
+        for (int j = 0; j < PTS; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
+        fwht_points<NT, PTS>(x, sx);
 #pragma unroll
-    for (int j = 0; j < PTS; j++) elds[t + NT * j] = mod65535(x[j] + (int)a.e_k);
-}
+        for (int j = 0; j < PTS; j++) elds[t + NT * j] = mod65535(x[j] + (int)a.e_k);
+    }
+};
 
 // The formal derivative (Engine::formal_derivative, src/engine.rs:233-238) of
 // the whole column, in the closed form out[j] = d[j] ^ XOR{ d[j | 2^b] : bit b
@@ -495,15 +506,44 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     // load while one is in flight: the decoder's polynomial starts once the
     // tables are in)
     auto dma_tables = [&]() {
-        if constexpr (L == 11) {
-            constexpr int G0 = ColSmem<11>::G0;
-            dma_copy<NT>(a.img_ifft + G0 * 80, smem + ColSmem<L>::A, (N - 1 - G0) * 80);
-            dma_copy<NT>(a.img_fft + G0 * 80, smem + ColSmem<L>::B, (N - 1 - G0) * 80);
-        } else {
-            dma_copy<NT>(a.img_ifft, smem + ColSmem<L>::A, (N - 1) * 80);
-            dma_copy<NT>(a.img_fft + (N / 2) * 80, smem + ColSmem<L>::B, (N / 2 - 1) * 80);
-        }
+        constexpr int G0 = ColSmem<L>::G0;
+        dma_copy<NT>(a.img_ifft + G0 * 80, smem + ColSmem<L>::A, (N - 1 - G0) * 80);
+        dma_copy<NT>(a.img_fft + G0 * 80, smem + ColSmem<L>::B, (N - 1 - G0) * 80);
     };
+    // ---- the decoder's erasure data first: the gather rows' received flags,
+    // the polynomial's inputs (EVAL) or eval_poly's output (EWORK), issued
+    // ahead of the row loads and the table DMA so that the polynomial can
+    // start as soon as they land (a wait for them would otherwise include
+    // every DMA issued before them; vmcnt counts in issue order)
+    [[maybe_unused]] uint8_t fr[4] = {0, 0, 0, 0};
+    [[maybe_unused]] ColEval<L, (DEC && EVAL) ? (GEN ? 4 : 8) : 1> ce;
+    [[maybe_unused]] uint32_t zv[2][4];
+    if constexpr (DEC) {
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            // (branch-free: rows outside both segments read a zero byte)
+            const uint32_t r = 4 * t + m;
+            const bool in_a = r < a.in_rows, in_b = GEN && r >= a.chunk && r - a.chunk < a.o_rows;
+            const uint8_t* fp = in_a && a.flags ? a.flags + r : (in_b && a.flags_o ? a.flags_o + (r - a.chunk) : a.zero);
+            fr[m] = *(const __attribute__((address_space(1))) uint8_t*)fp;
+        }
+        if constexpr (EVAL) {
+            ce.load(a);
+        } else if constexpr (L >= 9) {
+            const uint32_t w = t >> 6, lane = t & 63;
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) zv[b][j] = a.elog[(2 * w + b) * 256 + lane + 64 * j];
+        }
+    }
+    // the tables of the first IFFT block and the last FFT block (layers 0
+    // and 1, one thread each) straight into registers (L = 11: at their blocks)
+    BlockTabs ta, tb, t01f;
+    if constexpr (L <= 10) {
+        load_tabs01_img<L>(ta, t, a.img_ifft);
+        load_tabs01_img<L>(t01f, t, a.img_fft);
+    }
     uint32_t XL[4], XH[4];
 #pragma unroll
     for (int m = 0; m < 4; m++) {
@@ -518,7 +558,11 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         XL[m] = p[0];
         XH[m] = p[8];
     }
-    dma_tables();
+    // (the encoder stages its tables now; the decoder after its polynomial:
+    // with an LDS-DMA load in flight, the compiler makes a use of any
+    // ordinary load -- and a workgroup barrier -- wait for every load, DMA
+    // included, and the polynomial needs both)
+    if constexpr (!DEC) dma_tables();
     uint32_t gt[DEC ? 4 : 1][20];
     uint32_t ev[4] = {0, 0, 0, 0};
     bool lost[4] = {false, false, false, false};  // (GEN: the row is a lost original)
@@ -527,27 +571,24 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             const uint32_t r = 4 * t + m;
-            rcv[m] = r < a.in_rows && (!a.flags || a.flags[r] != 0);
+            rcv[m] = r < a.in_rows && (!a.flags || fr[m] != 0);
             if (GEN && a.rev_a && r < a.in_rows) lost[m] = !rcv[m];  // (low rate: originals = segment A)
             if (GEN && r >= a.chunk && r - a.chunk < a.o_rows) {
-                rcv[m] = !a.flags_o || a.flags_o[r - a.chunk] != 0;
+                rcv[m] = !a.flags_o || fr[m] != 0;
                 if (!a.rev_a) lost[m] = !rcv[m];
             }
         }
         uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
         if constexpr (EVAL) {
-            col_eval<L, GEN ? 4 : 8>(a, elds);
+            ce.prep(a);
+            ce.run(a, elds);
             __syncthreads();
         } else if constexpr (L >= 9) {
             // eval_poly's output before its last 256-point FWHT (a.elog = the
-            // engine's ework): wave w finishes the blocks of rows [512 w, 512 w + 512)
-            // (src/engine.rs:207-218) into LDS, for the work rows this codec reads
-            uint32_t zv[2][4];
+            // engine's ework, loaded above): wave w finishes the blocks of rows
+            // [512 w, 512 w + 512) (src/engine.rs:207-218) into LDS, for the
+            // work rows this codec reads
             const uint32_t w = t >> 6, lane = t & 63;
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) zv[b][j] = a.elog[(2 * w + b) * 256 + lane + 64 * j];
 #pragma unroll
             for (int b = 0; b < 2; b++) {
                 fwht256_wave(zv[b]);
@@ -564,6 +605,9 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             glb_table(gt[m], a.mul_tab, rcv[m] ? elds[a.base_in + r] : ZERO_ENTRY);
             ev[m] = elds[a.base_out + r];
         }
+        // the tables stream in behind the gather multipliers' loads (the
+        // multiply below waits for both)
+        dma_tables();
     }
     cstamp(a, 1);
     if constexpr (DEC) {
@@ -575,24 +619,23 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             XH[m] = zh;
         }
     }
-    __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads have landed)
-    __syncthreads();
+    if constexpr (L == 11) {
+        __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads have landed)
+        __syncthreads();
+    }
     cstamp(a, 2);
-    // the FFT's layer-0 tables into C (the decoder's logs there are read)
-    if constexpr (L <= 10) dma_copy<NT>(a.img_fft, smem + ColSmem<L>::C, (N / 2) * 80);
 
     // ---- IFFT (layers 0 .. L-1) then FFT (L-1 .. 0) in radix-4 blocks; the
     // next block's tables are read before each exchange.  Row bits 0-5 are
     // lane bits of some block (in-wave exchanges); from L = 9 on the top ones
     // are wave bits (two LDS exchanges); L = 7 ends with a one-layer block on
     // bits (4, 6).
-    BlockTabs ta, tb;
   if constexpr (L == 11) {
     // the general decoder over 2^11 work rows (8 waves; row bits 6-10 of
     // some blocks are wave bits: four LDS exchanges, the last IFFT / first
     // FFT layer as a one-layer block on bits (8, 10))
     static_assert(GEN, "2^11 rows: the general decoder only");
-    load_tabs01_img(ta, t, a.img_ifft);
+    load_tabs01_img<L>(ta, t, a.img_ifft);
     compute<false, true, true>(XL, XH, ta);
     cstamp(a, 3);
     load_tabs<L, false, 2, 3, true, true>(tb, t, smem);
@@ -632,12 +675,13 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     load_tabs<L, true, 2, 3, true, true>(tb, t, smem);
     wave_exchange<2, 3>(XL, XH);
     compute<true, true, true>(XL, XH, tb);
-    load_tabs01_img(tb, t, a.img_fft);
+    load_tabs01_img<L>(tb, t, a.img_fft);
     wave_exchange<0, 1>(XL, XH);
     cstamp(a, 8);
   } else {
-    load_tabs<L, false, 0, 1, true, true>(ta, t, smem);
-    compute<false, true, true>(XL, XH, ta);
+    compute<false, true, true>(XL, XH, ta);  // (layers 0, 1: tables from registers)
+    __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
+    __syncthreads();
     cstamp(a, 3);
     load_tabs<L, false, 2, 3, true, true>(tb, t, smem);
     wave_exchange<0, 1>(XL, XH);
@@ -675,8 +719,6 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
         } else if constexpr (L == 10) {
             load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
-            __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
-            __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
             exchange<6, 7, 8, 9>(XL, XH, t, smem);
             compute<false, true, true>(XL, XH, ta);
             cstamp(a, 5);
@@ -689,8 +731,6 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             exchange<8, 9, 6, 7>(XL, XH, t, smem);
         } else {
             load_tabs<L, false, 7, 8, false, true>(ta, t, smem);
-            __builtin_amdgcn_s_waitcnt(0);  // (C's LDS-DMA loads have landed: published by this barrier)
-            __syncthreads();  // (every wave is done with the IFFT's layer-0 tables under the image)
             exchange<6, 7, 7, 8>(XL, XH, t, smem);
             compute<false, false, true>(XL, XH, ta);
             cstamp(a, 5);
@@ -711,13 +751,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     load_tabs<L, true, 2, 3, true, true>(tb, t, smem);
     wave_exchange<2, 3>(XL, XH);
     compute<true, true, true>(XL, XH, tb);
-    if constexpr (L <= 8) {
-        // (no barrier since the staging one: the FFT's layer-0 tables in C
-        // must have landed and be visible before the last block reads them)
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-    }
-    load_tabs<L, true, 0, 1, true, true>(tb, t, smem);
+    tb = t01f;  // (layers 1, 0: tables from registers)
     wave_exchange<0, 1>(XL, XH);
     cstamp(a, 8);
   }
