@@ -597,6 +597,31 @@ def main():
                                           "encode_us_per_call": tb / nt * 1e6,
                                           "decode_100pct_gib_s": world * nb * 2 * kb * S * nt / td / GIB,
                                           "decode_us_per_call": td / nt * 1e6, "stripes_per_call": nb}
+            if kb == 1000:
+                # every stripe with a loss set of its own (rs16_decode_device_batch_varied):
+                # stripe i loses a random half of its originals and receives as
+                # many random recovery shards; restore checked on every stripe
+                rng = np.random.default_rng(7)
+                fo_h = np.ones((nb, kb), np.uint8)
+                fr_h = np.zeros((nb, kb), np.uint8)
+                for i in range(nb):
+                    fo_h[i, rng.choice(kb, kb // 2, replace=False)] = 0
+                    fr_h[i, rng.choice(kb, kb // 2, replace=False)] = 1
+                held = np.tile(ob.reshape(1, kb, S), (nb, 1, 1))
+                held[fo_h == 0] = 0
+                dv = DeviceArray.from_numpy(eng, held.reshape(-1))
+                dfo, dfr = DeviceArray.from_numpy(eng, fo_h.reshape(-1)), DeviceArray.from_numpy(eng, fr_h.reshape(-1))
+                oc, rc = [int(x) for x in fo_h.sum(1)], [int(x) for x in fr_h.sum(1)]
+                dvf = lambda: rs16.decode_device_batch_varied(kb, kb, S, nb, dv.ptr, kb * S, dfo.ptr, kb, db_r.ptr,
+                                                              kb * S, dfr.ptr, kb, oc, rc, engine=eng)
+                dvf()
+                back = dv.download(shape=(nb, kb, S))
+                assert all(np.array_equal(back[i], ob) for i in range(nb)), "varied batched decode did not restore"
+                tv = timed(dvf, nt)
+                bat[f"{kb}:{kb}x{S}x{nb}"].update({
+                    "decode_varied_gib_s": world * nb * 2 * kb * S * nt / tv / GIB,
+                    "decode_varied_us_per_call": tv / nt * 1e6,
+                    "decode_varied": "every stripe its own random loss of half its originals (general decode)"})
         extra["batched_stripes"] = bat
 
     if not args.no_extra and loss >= 100:

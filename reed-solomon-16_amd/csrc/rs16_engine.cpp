@@ -673,6 +673,18 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.in2 = U;
     a.out = nullptr;
     a.tile_base = t0;
+    // Few lost originals (lost-range pruning leaves a handful of tiles to
+    // this pass): one wave per quad column of each tile (tile_last_kernel)
+    // instead of one 8-wave item per 32 quads, whose latency was the pass.
+    const size_t lost = g.high ? (size_t)g.b_count - g.b_recv : (size_t)g.a_count - g.a_recv;
+    const bool tile_last = lo == 8 && !(g_diag & DIAG_NO_TILE_LAST) && (lost <= 2048 || (g_diag & DIAG_TILE_LAST));
+    if (tile_last) {
+        const uint32_t tiles = batch(t1 - t0, zs, zs, 0);
+        hipEvent_t ev;
+        if (int rc = prof_begin(s, &ev, err)) return rc;
+        RS16_HIP(launch_tile_last(a, tiles, s));
+        return prof_end(DEC_LAST, s, ev, err);
+    }
     RS16_PASS(DEC_LAST, lo, a, batch(t1 - t0, zs, zs, 0), s);
     return RS16_OK;
 }

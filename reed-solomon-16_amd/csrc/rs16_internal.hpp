@@ -232,6 +232,8 @@ enum DiagFlags : int {
     DIAG_EVAL_FULL = 4,       // eval_poly: the full 65536-point form even for n <= 2048
     DIAG_NO_COLUMN = 8,       // 2^9 / 2^10-row transforms through the pass codec (rs16_col.hip off)
     DIAG_FORCE_COLUMN = 16,   // ... through the column codec at any width (rs16_engine::col_max_quads ignored)
+    DIAG_TILE_LAST = 32,      // the general decode's T = 8 last pass as tile_last_kernel at any loss count
+    DIAG_NO_TILE_LAST = 64,   // ... always as the 8-wave pass (DEC_LAST items)
 };
 extern int g_diag;
 
@@ -239,6 +241,10 @@ constexpr size_t RS16_ZERO_BYTES = 65536;
 
 // Launch `num_tiles` tiles (x nslab slabs) of program P with tile bits T.
 hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, hipStream_t s);
+// DEC_LAST at T = 8 as one wave per quad column of a tile (rs16_pass.hip
+// tile_last_kernel): `num_tiles` tiles (x stripes, PassArgs::stripe_tiles)
+// from a.tile_base, rows at lo = 0.
+hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s);
 
 // Elementwise / small kernels.
 hipError_t launch_mul(uint8_t* x, size_t bytes, uint32_t entry, const uint32_t* mul_tab, hipStream_t s);

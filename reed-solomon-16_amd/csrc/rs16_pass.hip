@@ -57,6 +57,7 @@
 //   tile within the stripe) and the stripe displaces its array pointers.
 #include "rs16_internal.hpp"
 #include "rs16_fwht.hpp"
+#include "rs16_colops.hpp"
 
 namespace rs16 {
 
@@ -1332,6 +1333,183 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     st.template finish<EARLY>(a, c, smem);
     stamp(a, 2);
     process_item<P, T>(a, c, tile, slab, cur, smem);
+}
+
+// ---------------------------------------------------------------------------
+// The general decode's last pass (DEC_LAST: y = u + L(z) -> FFT of the tile's
+// 8 low row bits -> reveal x (65535 - e) -> store the lost originals,
+// rate_high.rs:232-242 / rate_low.rs:232-242) as one wave per quad column of
+// a 256-row tile instead of one 8-wave workgroup per (tile, 32-quad slab):
+// lane l holds 4 rows of its quad column, the FFT runs in 4 radix-4 blocks
+// in registers with in-wave row-bit exchanges (colops, as the column codec
+// at 256 rows), the in-tile formal-derivative terms come from registers and
+// lane shuffles (no LDS image, no barrier).  Four quad columns per
+// workgroup share the tile's 255 twiddle tables (staged by LDS-DMA once) and
+// the tile's erasure logs.  A decode that lost few originals needs this pass
+// for a handful of tiles only (lost-range pruning): there the 8-wave item's
+// latency (two waves per SIMD through 8 layers of 16 rows) was the whole
+// pass, 25 us for the reference bench's 1 % loss; here each wave carries a
+// quarter of the rows.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
+    using namespace colops;
+    constexpr int T = 8;
+    constexpr uint32_t NTAB = (1u << T) - 1;
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[NTAB * 80];
+    __shared__ uint32_t elds[256];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = uni(t >> 6);
+    const uint32_t nq4 = (a.qrow + 3) / 4;
+    uint32_t tile = blockIdx.x / nq4;
+    const uint32_t qg = blockIdx.x - tile * nq4;
+    if (a.stripe_tiles) {
+        const uint32_t st = uni(tile / a.stripe_tiles);
+        tile -= st * a.stripe_tiles;
+        a.in += st * a.bs_in;
+        a.in2 += st * a.bs_in2;
+        a.rest += st * a.bs_rest;
+        if (a.flags_a) a.flags_a += st * a.bs_fa;
+        if (a.flags_b) a.flags_b += st * a.bs_fb;
+        if (a.elog) a.elog += st * a.bs_elog;
+        if (a.ework) a.ework += st * a.bs_elog;
+        if (a.zflags) a.zflags += st * a.bs_zflags;
+        if (a.lostrange) a.lostrange += st * a.bs_lost;
+    }
+    tile += a.tile_base;
+    if (a.lostrange) {
+        // a tile without a lost original stores nothing
+        const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
+        if (!((tile << T) < r1 && ((tile + 1) << T) > r0)) return;
+    }
+    const uint32_t q = qg * 4 + w;
+    const bool active = q < a.qrow;
+    const uint32_t offL = (q >> 3) * 64 + (q & 7) * 4;
+    const bool ztile = a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u);
+    // ---- requests: z and u of the lane's rows in the first FFT block's
+    // layout (row bits 6, 7 in registers: row k = lane + 64 m), the tile's
+    // erasure-log block (wave 0, when eval_poly left its last H_lo to this
+    // pass), then the twiddle tables by LDS-DMA
+    uint32_t ZL[4], ZH[4], YL[4], YH[4];
+    const uint8_t* zpage = a.zero + (offL & 0x7FFFu);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const uint64_t r = ((uint64_t)tile << T) + lane + 64u * m;
+        const uint32_t* pz = (const uint32_t*)(active && !ztile ? a.in + r * a.S_in + offL : zpage);
+        const uint32_t* pu = (const uint32_t*)(active ? a.in2 + r * a.S_in + offL : zpage);
+        ZL[m] = pz[0];
+        ZH[m] = pz[8];
+        YL[m] = pu[0];
+        YH[m] = pu[8];
+    }
+    const uint32_t row0 = (tile << T) + a.row_base_out;  // the tile's first decode work row
+    uint32_t ev[4] = {0, 0, 0, 0};
+    if (a.ework && w == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) ev[j] = a.ework[(row0 & ~255u) + lane + 64u * j];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i * 256 < NTAB * 5; i++) {
+        const uint32_t c = i * 256 + t;
+        if (c < NTAB * 5) {
+            // chunk c = part c % 5 of table tb = c / 5 (tile-group order: layer
+            // kb at groups [2^T - 2^(T-kb), ...), group j = row >> (kb + 1))
+            const uint32_t tb = c / 5, part = c - tb * 5;
+            const uint32_t kb = (uint32_t)(T - 32 + __clz(NTAB - tb));
+            const uint32_t j = tb - ((1u << T) - (1u << (T - kb)));
+            const uint32_t idx = (tile << T) + (j << (kb + 1)) + (1u << kb) + a.skew_fft - 1;
+            __builtin_amdgcn_global_load_lds((colops::glb_vp)(a.skew_tab + (size_t)idx * TAB_DWORDS + part * 4),
+                                             (colops::lds_vp)(tabs + (i * 256 + 64 * w) * 16), 16, 0, 0);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    if (a.ework && w == 0) {
+        fwht256_wave(ev);  // the last 256-point FWHT of eval_poly (src/engine.rs:207-218)
+#pragma unroll
+        for (int j = 0; j < 4; j++) elds[lane + 64 * j] = ev[j];
+    }
+    __syncthreads();  // tables and logs in LDS
+    // ---- reveal multipliers of the lane's output rows (the last block's
+    // layout: row k = 4 lane + m), requested now, used after the FFT
+    uint32_t rt[4][20];
+    bool lost[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const uint32_t r = row0 + 4 * lane + m;
+        lost[m] = active && row_lost_original(a, r);
+        const uint32_t e = a.ework ? elds[(4 * lane + m + row0) & 255u] : (lost[m] ? a.elog[r] : 0u);
+        glb_table(rt[m], a.mul_tab, lost[m] ? GF_MODULUS - e : ZERO_ENTRY);
+    }
+    // ---- y = u + L(z): the formal derivative's terms of the tile's row bits
+    // (src/engine.rs:233-238 in closed form): y[k] ^= z[k | 2^b] for every
+    // bit b < 8 that is 0 in k -- bits 6, 7 are register bits, 0-5 lane bits
+    if (!ztile) {
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            if (!(m & 1)) YL[m] ^= ZL[m | 1], YH[m] ^= ZH[m | 1];
+            if (!(m & 2)) YL[m] ^= ZL[m | 2], YH[m] ^= ZH[m | 2];
+        }
+#define RS16_FDL(B)                                                                   \
+        {                                                                             \
+            const bool take = !(lane & (1u << (B)));                                  \
+            _Pragma("unroll") for (int m = 0; m < 4; m++) {                           \
+                const uint32_t pl = (uint32_t)xshfl<(1 << (B))>((int)ZL[m]);          \
+                const uint32_t ph = (uint32_t)xshfl<(1 << (B))>((int)ZH[m]);          \
+                YL[m] ^= take ? pl : 0u;                                              \
+                YH[m] ^= take ? ph : 0u;                                              \
+            }                                                                         \
+        }
+        RS16_FDL(0) RS16_FDL(1) RS16_FDL(2) RS16_FDL(3) RS16_FDL(4) RS16_FDL(5)
+#undef RS16_FDL
+    }
+    // ---- FFT of the tile's 8 row bits, high layers first: blocks (6, 7),
+    // (4, 5), (2, 3), (0, 1)
+    auto tabs_of = [&](BlockTabs& bt, auto b0c, auto b1c) {
+        constexpr int B0 = decltype(b0c)::value, B1 = decltype(b1c)::value;
+        const uint32_t r0 = brow<B0, B1>(lane, 0), r2 = brow<B0, B1>(lane, 2);
+        auto off = [](int kb, uint32_t r) { return (((1u << T) - (1u << (T - kb))) + (r >> (kb + 1))) * 80u; };
+        lds_table(bt.w0, tabs, off(B0, r0));
+        lds_table(bt.w2, tabs, off(B0, r2));
+        lds_table(bt.w1, tabs, off(B1, r0));
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using I5 = std::integral_constant<int, 5>;
+    using I6 = std::integral_constant<int, 6>;
+    using I7 = std::integral_constant<int, 7>;
+    BlockTabs ta, tb;
+    tabs_of(ta, I6(), I7());
+    tabs_of(tb, I4(), I5());
+    compute<true, true, true>(YL, YH, ta);
+    wave_exchange<4, 5>(YL, YH);
+    tabs_of(ta, I2(), I3());
+    compute<true, true, true>(YL, YH, tb);
+    wave_exchange<2, 3>(YL, YH);
+    tabs_of(tb, I0(), I1());
+    compute<true, true, true>(YL, YH, ta);
+    wave_exchange<0, 1>(YL, YH);
+    compute<true, true, true>(YL, YH, tb);
+    // ---- reveal (x (65535 - e)) and store the lost originals in place
+    // (restored-originals row = work row - the originals' segment start)
+    const int64_t shift = (int64_t)a.row_base_out - (a.rest_seg_b ? (int64_t)a.chunk : 0);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        if (!lost[m]) continue;
+        uint32_t ol = 0, oh = 0;
+        mul_xor(ol, oh, YL[m], YH[m], rt[m]);
+        const int64_t rr = (int64_t)(tile << T) + 4 * lane + m + shift;
+        uint32_t* p = (uint32_t*)(a.rest + rr * (int64_t)a.S_rest + offL);
+        __builtin_nontemporal_store(ol, p);
+        __builtin_nontemporal_store(oh, p + 8);
+    }
+}
+
+hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s) {
+    if (num_tiles == 0 || a.qrow == 0) return hipSuccess;
+    const uint32_t nwg = num_tiles * ((a.qrow + 3) / 4);
+    hipLaunchKernelGGL(tile_last_kernel, dim3(nwg), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -42,3 +42,24 @@ eng.synchronize()
 prof = eng.profile()
 eng.set_profiling(False)
 print("1 % decode per pass (us):", {n: round(ms * 1e3 / max(c, 1), 2) for n, (ms, c) in prof.items() if c})
+
+# the last pass in both forms (identical results)
+for name, flag in (("tile_last", rs16.DIAG_TILE_LAST), ("items", rs16.DIAG_NO_TILE_LAST)):
+    old = rs16.set_diagnostics(flag)
+    x.upload(o1)
+    eng.set_profiling(True)
+    eng.profile_reset()
+    for _ in range(10):
+        rs16.decode_device(k, m, S, x.ptr, a.ptr, d_r.ptr, b.ptr, k - 327, 327, engine=eng)
+    eng.synchronize()
+    prof = eng.profile()
+    eng.set_profiling(False)
+    ok = np.array_equal(x.download(shape=(k, S)), orig)
+    t = time.perf_counter()
+    for _ in range(50):
+        rs16.decode_device(k, m, S, x.ptr, a.ptr, d_r.ptr, b.ptr, k - 327, 327, engine=eng)
+    eng.synchronize()
+    us = (time.perf_counter() - t) / 50 * 1e6
+    rs16.set_diagnostics(old)
+    print(name, "exact:", ok, "loop us/call:", round(us, 1), "GiB/s:", round(2 * k * S / us / 1e-6 / 2**30, 1),
+          {n: round(ms * 1e3 / max(c, 1), 2) for n, (ms, c) in prof.items() if c}, flush=True)

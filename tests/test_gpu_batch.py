@@ -214,3 +214,16 @@ def test_decode_batch_varied_errors():
         rs16.decode_device_batch_varied(2, 2, 64, 2, d.ptr, 128, f.ptr, 1, d.ptr, 128, f.ptr, 2, [1, 1], [1, 1],
                                         engine=eng)
     assert e.value.kind == "InvalidArgument"
+
+
+@pytest.mark.parametrize("diag", ["DIAG_TILE_LAST", "DIAG_NO_TILE_LAST"])
+@pytest.mark.parametrize("mode", ["mixed", "scatter"])
+def test_decode_batch_varied_last_pass_paths(diag, mode):
+    # the 65536-row varied decode with its last pass forced to each form
+    # (tile_last_kernel with per-stripe lost ranges / zero tiles, and the
+    # 8-wave items)
+    old = rs16.set_diagnostics(getattr(rs16, diag))
+    try:
+        test_decode_batch_varied(32768, 32768, 64, 3, mode)
+    finally:
+        rs16.set_diagnostics(old)

@@ -249,3 +249,37 @@ def test_decode_lost_range_pruning(eng, k, m, sb, pattern):
     recovery = dev_encode(eng, original, m)
     om, rm = lost_pattern(k, m, pattern)
     assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+
+
+@pytest.mark.parametrize("path", ["tile", "items"])
+@pytest.mark.parametrize("k,m,sb,pattern", [
+    (32768, 32768, 1024, "tail"),      # the reference bench's 1 % loss (benches/benchmarks.rs:84-87)
+    (32768, 32768, 64 * 5, "two"),     # partial 64-byte blocks of a workgroup's 4 quad columns
+    (32768, 32768, 64, "edge"),
+    (30000, 3000, 192, "tail"),        # high rate, k > m (a zero tail in the decode work)
+    (3000, 30000, 64, "one_mid"),      # low rate: originals are segment A
+    (32768, 32768, 128, "blocks"),     # zero DEC_FIRST tiles next to tiles with lost originals
+    (32768, 32768, 64, "scatter"),     # every tile holds lost originals
+])
+def test_decode_last_pass_paths(eng, k, m, sb, pattern, path):
+    # The general decode's last pass over 65536 work rows in both forms: one
+    # wave per quad column of a tile (tile_last_kernel, the default for few
+    # lost originals) and 8-wave items of 32 quad columns -- forced here
+    # either way for every pattern; bit-exact restoration, received
+    # originals untouched
+    original = generate_original(k, sb, 17)
+    recovery = dev_encode(eng, original, m)
+    if pattern == "blocks":
+        om, rm = loss_masks(k, m, "blocks")
+    elif pattern == "scatter":
+        om = np.ones(k, bool)
+        om[np.random.default_rng(5).choice(k, min(k, m) // 2, replace=False)] = False
+        rm = np.zeros(m, bool)
+        rm[:int((~om).sum())] = True
+    else:
+        om, rm = lost_pattern(k, m, pattern)
+    old = rs16.set_diagnostics(rs16.DIAG_TILE_LAST if path == "tile" else rs16.DIAG_NO_TILE_LAST)
+    try:
+        assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+    finally:
+        rs16.set_diagnostics(old)
