@@ -415,7 +415,8 @@ enum {
     RS16_DIAG_FORCE_COLUMN = 16,   /* ... through the column codec at any shard width / stripe count */
     RS16_DIAG_TILE_LAST = 32,      /* the general decode's last pass (65536 work rows) one wave per quad
                                       column of a tile at any loss count (default: <= 2048 lost) */
-    RS16_DIAG_NO_TILE_LAST = 64    /* ... always as 8-wave items of 32 quad columns */
+    RS16_DIAG_NO_TILE_LAST = 64,   /* ... always as 8-wave items of 32 quad columns */
+    RS16_DIAG_FD_LDS = 128         /* the general decode's in-tile formal derivative always through LDS */
 };
 int rs16_set_diagnostics(int flags);
 

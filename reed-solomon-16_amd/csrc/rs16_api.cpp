@@ -145,7 +145,7 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
 extern "C" int rs16_set_diagnostics(int flags) {
     const int old = g_diag;
     g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN |
-                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST);
+                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS);
     return old;
 }
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }

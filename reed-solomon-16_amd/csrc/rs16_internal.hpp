@@ -121,6 +121,7 @@ struct PassArgs {
     // rows straddle the decoder's segment boundary, so HBM addresses are an
     // SGPR row base + a 32-bit lane offset (else 64-bit lane offsets).
     uint32_t voff32;
+    uint32_t fd_lds;  // DEC_MID: in-tile formal derivative through LDS only (DIAG_FD_LDS)
     // Decode zero tiles: zflags[t] = 1 when DEC_FIRST tile t holds no received
     // row (then it is all zero after the erasure multiply and is neither
     // computed nor stored).  Written with rbits by the eval_poly kernels from
@@ -234,6 +235,7 @@ enum DiagFlags : int {
     DIAG_FORCE_COLUMN = 16,   // ... through the column codec at any width (rs16_engine::col_max_quads ignored)
     DIAG_TILE_LAST = 32,      // the general decode's T = 8 last pass as tile_last_kernel at any loss count
     DIAG_NO_TILE_LAST = 64,   // ... always as the 8-wave pass (DEC_LAST items)
+    DIAG_FD_LDS = 128,        // DEC_MID's in-tile formal derivative always through the LDS image (tile_fd)
 };
 extern int g_diag;
 

@@ -690,17 +690,65 @@ __device__ __forceinline__ void fd_rows(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)
 struct NoMid {
     __device__ __forceinline__ void operator()() const {}
 };
-template <int T, int NQR, bool FROM_B, class MID = NoMid>
+// `post` runs in the thread's own round after its rows are read (the image
+// of that round is still in place).
+template <int T, int NQR, bool FROM_B, class MID = NoMid, class POST = NoMid>
 __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
-                                         uint2* lds, MID mid = MID()) {
+                                         uint2* lds, MID mid = MID(), POST post = POST()) {
     constexpr int QL = Geo<T>::Q / NQR;
 #pragma unroll
     for (int r = 0; r < NQR; r++) {
         if (my_round<NQR>(c, r)) put_rows<T, QL, FROM_B>(L, H, c, lds);
         __syncthreads();
         if (r == 0) mid();
-        if (my_round<NQR>(c, r)) get_rows<T, QL, !FROM_B>(L, H, c, lds);
+        if (my_round<NQR>(c, r)) {
+            get_rows<T, QL, !FROM_B>(L, H, c, lds);
+            post();
+        }
         __syncthreads();
+    }
+}
+
+// DEC_MID's formal derivative split by row bits (the two-direction pass's
+// layers: IFFT bits [0, R) in layout A, bits [R, T) in layout B, then the
+// FFT back).  With w = the rows after the layout-A IFFT layers, z = M_B(w)
+// after the layout-B ones, and F_B the layout-B FFT layers (F_B M_B = I:
+// same twiddles, inverse butterflies), a term P_b (row k|2^b into row k,
+// k_b = 0) of a bit b < R commutes with the butterflies of bits above b, so
+//   F_B((I + sum_b P_b) z) = F_B((I + sum_{b >= R} P_b) z) + sum_{b < R} P_b w:
+// the terms of the layout-B bits come from registers after the layout-B
+// IFFT layers (fd_regs), those of the layout-A bits from the image of w that
+// the first layout switch writes anyway (fd_image, read in the switch), and
+// they are added to the FFT's rows after its layout-B layers.  No LDS round
+// of its own, no barrier.  (DEC_LAST's y = u + L(z) is the same identity one
+// pass up: tile_last_kernel.)
+template <int T>
+__device__ __forceinline__ void fd_regs(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR]) {
+    constexpr int R = Geo<T>::R, SHB = Geo<T>::SHB;
+#pragma unroll
+    for (int m = 0; m < Geo<T>::NR; m++) {
+#pragma unroll
+        for (int b = R; b < T; b++) {
+            const int mb = b - SHB;  // layout B: k = s + (m << SHB)
+            if (!((m >> mb) & 1)) {  // the source row m | 2^mb is updated later
+                L[m] ^= L[m | (1 << mb)];
+                H[m] ^= H[m | (1 << mb)];
+            }
+        }
+    }
+}
+// XOR_{b < R, k_b = 0} w[k | 2^b] from the image of w (any layout: the image
+// is indexed by tile row)
+template <int T, int QL>
+__device__ __forceinline__ void fd_image(uint32_t& dl, uint32_t& dh, const Thr& c, const uint2* lds, uint32_t k) {
+    dl = dh = 0;
+#pragma unroll
+    for (int b = 0; b < Geo<T>::R; b++) {
+        const uint32_t* p = Img<T, QL>::at((uint2*)lds, c, k | (1u << b));
+        const uint32_t vl = p[0], vh = p[Img<T, QL>::PLANE];
+        const bool take = !((k >> b) & 1);
+        dl ^= take ? vl : 0u;
+        dh ^= take ? vh : 0u;
     }
 }
 
@@ -1114,6 +1162,24 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     constexpr bool START_B = !PT::IFFT;
     // Final layout: after FFT -> A; after IFFT only -> B (T > 4); T <= 4: A == B.
     [[maybe_unused]] constexpr bool END_B = !PT::FFT && T > 4;
+    // DEC_MID whose consumed tile rows (the last pass's tiles with a lost
+    // original, [need_lo, need_hi)) lie in few layout-B register rows: the
+    // formal derivative split by row bits (fd_regs / fd_image), otherwise
+    // through the LDS image (tile_fd).  The layout-A FFT layers make every
+    // row of a consumed row's 2^R-row block an input of it: the block's
+    // layout-B register rows [fd_m0, fd_m0 + FD_ND) take the fd_image terms.
+    constexpr bool SPLIT_FD = P == DEC_MID && T > 4;
+    constexpr int FD_PB = 1 << (R - G::SHB);            // register rows per 2^R-row block
+    constexpr int FD_ND = FD_PB > 2 ? FD_PB : 2;        // register rows carried
+    [[maybe_unused]] bool fd_few = false;
+    [[maybe_unused]] uint32_t fd_m0 = 0;
+    [[maybe_unused]] uint32_t dl[FD_ND], dh[FD_ND];
+    if constexpr (SPLIT_FD) {
+        const uint32_t lo = uni(a.need_lo), hi = uni(min(a.need_hi, 1u << T));
+        const uint32_t m0 = (lo >> R) * FD_PB, m1 = hi <= lo ? m0 : (((hi - 1) >> R) + 1) * FD_PB;
+        fd_few = !a.fd_lds && m1 - m0 <= (uint32_t)FD_ND;
+        fd_m0 = hi <= lo ? 0u : min(m0, (uint32_t)(NR - FD_ND));
+    }
 
     if constexpr (P == DEC_FIRST) {
         // A tile without received rows is zero after the erasure multiply
@@ -1149,9 +1215,21 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         if constexpr (T > 4) {
             Stager<T, (LateS2<P, T>::value ? G::TSPLIT : 0)> s3;
             if constexpr (LateS2<P, T>::value) s3.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
-            exchange<T, NQR, false>(L, H, c, lds, [&]() {
-                if constexpr (LateS2<P, T>::value) s3.commit((uint4*)(smem + SM::TAB1_OFF));
-            });
+            exchange<T, NQR, false>(
+                L, H, c, lds,
+                [&]() {
+                    if constexpr (LateS2<P, T>::value) s3.commit((uint4*)(smem + SM::TAB1_OFF));
+                },
+                [&]() {
+                    if constexpr (SPLIT_FD) {
+                        if (fd_few) {
+                            constexpr int QL = G::Q / NQR;
+#pragma unroll
+                            for (int i = 0; i < FD_ND; i++)
+                                fd_image<T, QL>(dl[i], dh[i], c, lds, kidx<T, true>(c, fd_m0 + i));
+                        }
+                    }
+                });
             stamp(a, 4);
             layers<P, T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
                                                                                                 tab2, d.zmask);
@@ -1162,8 +1240,13 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     }
     // ---------------- formal derivative (tile bits) ----------------
     if constexpr (PT::FD) {
-        if (in_b) tile_fd<T, NQR, true>(L, H, L, H, c, lds);
-        else tile_fd<T, NQR, false>(L, H, L, H, c, lds);
+        if constexpr (SPLIT_FD) {
+            if (fd_few) fd_regs<T>(L, H);
+            else tile_fd<T, NQR, true>(L, H, L, H, c, lds);
+        } else {
+            if (in_b) tile_fd<T, NQR, true>(L, H, L, H, c, lds);
+            else tile_fd<T, NQR, false>(L, H, L, H, c, lds);
+        }
         stamp(a, 6);
     }
     // ---------------- FFT ----------------
@@ -1171,6 +1254,18 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         if constexpr (T > 4) {
             layers<P, T, true, R, (T > 4 ? T : R), true, TWO, (P == DEC_MID ? PR_OUT : PR_NONE)>(L, H, c, a, tab1,
                                                                                              tab2);
+            if constexpr (SPLIT_FD) {
+                // the layout-A bits' derivative terms (fd_image) join the
+                // register rows that feed consumed rows
+                if (fd_few) {
+#pragma unroll
+                    for (int m = 0; m < NR; m++) {
+#pragma unroll
+                        for (int i = 0; i < FD_ND; i++)
+                            if ((uint32_t)m == fd_m0 + i) L[m] ^= dl[i], H[m] ^= dh[i];
+                    }
+                }
+            }
             stamp(a, 7);
             prio<P, 3, T>();
             // reveal multipliers: requested before the last layout switch,
@@ -1561,6 +1656,7 @@ hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles
         const bool aligned = a.chunk % span == 0 && a.row_base_in % span == 0;
         // (rs16_set_diagnostics RS16_DIAG_FORCE_VOFF64: always the 64-bit lane offsets)
         a.voff32 = fits && aligned && !(g_diag & DIAG_FORCE_VOFF64) ? 1u : 0u;
+        a.fd_lds = (g_diag & DIAG_FD_LDS) ? 1u : 0u;
     }
     const size_t lds = (size_t)kSmem[prog][T];
     if (lds > 65536) {

@@ -44,7 +44,7 @@ eng.set_profiling(False)
 print("1 % decode per pass (us):", {n: round(ms * 1e3 / max(c, 1), 2) for n, (ms, c) in prof.items() if c})
 
 # the last pass in both forms (identical results)
-for name, flag in (("tile_last", rs16.DIAG_TILE_LAST), ("items", rs16.DIAG_NO_TILE_LAST)):
+for name, flag in (("default", 0), ("fd_lds", rs16.DIAG_FD_LDS), ("items", rs16.DIAG_NO_TILE_LAST)):
     old = rs16.set_diagnostics(flag)
     x.upload(o1)
     eng.set_profiling(True)
@@ -55,6 +55,9 @@ for name, flag in (("tile_last", rs16.DIAG_TILE_LAST), ("items", rs16.DIAG_NO_TI
     prof = eng.profile()
     eng.set_profiling(False)
     ok = np.array_equal(x.download(shape=(k, S)), orig)
+    for _ in range(30):  # back to full clocks after the download
+        rs16.decode_device(k, m, S, x.ptr, a.ptr, d_r.ptr, b.ptr, k - 327, 327, engine=eng)
+    eng.synchronize()
     t = time.perf_counter()
     for _ in range(50):
         rs16.decode_device(k, m, S, x.ptr, a.ptr, d_r.ptr, b.ptr, k - 327, 327, engine=eng)

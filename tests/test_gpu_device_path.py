@@ -283,3 +283,45 @@ def test_decode_last_pass_paths(eng, k, m, sb, pattern, path):
         assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
     finally:
         rs16.set_diagnostics(old)
+
+
+@pytest.mark.parametrize("fd", ["split", "lds"])
+@pytest.mark.parametrize("k,m,sb,diag,lost", [
+    # DEC_MID T = 8 (65536 work rows): a layout-B register row = 4096 originals
+    (32768, 32768, 64, 0, list(range(4090, 4102))),   # across a register-row boundary
+    (32768, 32768, 64, 0, [0, 8000]),                 # two adjacent register rows, sparse
+    (32768, 32768, 128, 0, [5000, 5001]),
+    (32768, 32768, 64, 0, [0, 12288]),                # three register rows: the LDS derivative
+    (32768, 32768, 64, 0, list(range(32768 - 327, 32768))),  # benches/benchmarks.rs:84-87, 1 %
+    # T = 7 (8192 work rows): register row = 512 originals
+    (4096, 4096, 128, 0, list(range(508, 516))),
+    (4096, 4096, 64, 0, [0, 1000]),
+    (4096, 4096, 64, 0, [0, 1100]),
+    # T = 6 (4096 work rows): register row = 256 originals
+    (2000, 2000, 64, 0, list(range(250, 261))),
+    (2000, 2000, 64, 0, [0, 300]),
+    (2000, 2000, 64, 0, [0, 600]),
+    # T = 5 through the pass codec (2^10 work rows): register row = 128 originals
+    (500, 500, 64, 8, list(range(120, 131))),
+    (500, 500, 64, 8, [0, 200]),
+    (500, 500, 64, 8, [0, 300]),
+    # high / low rate with a zero tail / zero prefix in the work
+    (30000, 3000, 64, 0, [10, 20, 4095, 4096]),
+    (3000, 30000, 64, 0, list(range(250, 261))),
+])
+def test_decode_split_formal_derivative(eng, k, m, sb, diag, lost, fd):
+    # DEC_MID's in-tile formal derivative split by row bits (fd_regs /
+    # fd_image, rs16_pass.hip) when the consumed tile rows lie in two
+    # layout-B register rows, else through the LDS image; DIAG_FD_LDS forces
+    # the LDS form everywhere.  Both restore the lost originals bit-exactly.
+    original = generate_original(k, sb, 19)
+    recovery = dev_encode(eng, original, m)
+    om = np.ones(k, bool)
+    om[lost] = False
+    rm = np.zeros(m, bool)
+    rm[:len(lost)] = True
+    old = rs16.set_diagnostics(diag | (rs16.DIAG_FD_LDS if fd == "lds" else 0))
+    try:
+        assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
+    finally:
+        rs16.set_diagnostics(old)
