@@ -553,10 +553,14 @@ def main():
         e2()
         d2()
         assert np.array_equal(x.download(shape=(k2, S)), o2)
-        for _ in range(args.warmup):
-            e2(); d2()
-        n2 = max(args.steps, 50)
+        # (steady state: each call kind warmed on its own, then >= 400 calls;
+        # a few dozen calls after a sync measure the launch latency instead)
+        n2 = max(10 * args.steps, 400)
+        for _ in range(50):
+            e2()
         te = timed(e2, n2)
+        for _ in range(50):
+            d2()
         td = timed(d2, n2)
         extra["1000:1000x1024"] = {"encode_gib_s": world * (k2 + m2) * S * n2 / te / GIB,
                                    "decode_gib_s": world * (k2 + m2) * S * n2 / td / GIB,

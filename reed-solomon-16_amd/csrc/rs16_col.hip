@@ -31,11 +31,14 @@
 //     around the block whose row bits are the wave index (two exchanges
 //     through an 8 KiB LDS image, XOR-swizzled so that the b64 accesses are
 //     bank-conflict free).
-//   * All 2 (2^L - 1) twiddle tables of the codec (80-byte v_perm tables,
-//     rs16_gf.hpp; 160 KiB at L = 10) are staged into LDS by LDS-DMA loads
-//     (global_load_lds_dwordx4) from contiguous images the engine builds at
-//     creation (HostTables::col_img): no VGPRs, no address arithmetic.  The
-//     FFT's last layer streams in while the IFFT runs.
+//   * The 2 (2^L - 1) twiddle tables of the codec (80-byte v_perm tables,
+//     rs16_gf.hpp) come from contiguous images the engine builds on first use
+//     (HostTables::col_img): those of layers 0 and 1 (3/4 of them, each used
+//     by one thread in one block) straight into the thread's registers, those
+//     of layers >= 2 into LDS by LDS-DMA loads (global_load_lds_dwordx4, no
+//     VGPRs, no address arithmetic; 40 KiB at L = 10) issued behind the row
+//     loads (the decoder: behind its polynomial, ColEval) so that the
+//     compiler's vmcnt waits on the rows do not drain the DMA.
 //   * The IFFT's last block and the FFT's first share their row bits: no
 //     exchange between the two directions.
 //   * Rows are loaded straight into the first block's layout and stored from
@@ -246,8 +249,8 @@ template <int NT, int PTS> __device__ __forceinline__ void fwht_points(int (&x)[
 // thread's points) -- the kernel calls it before its row loads and table
 // DMA, so that waiting for them does not wait for the DMA (vmcnt counts in
 // issue order) -- and run() computes.
-template <int L, int PTS> struct ColEval {
-    static constexpr int N = 1 << L, NT = N / 4;
+template <int L, int PTS, int NT_ = (1 << L) / 4> struct ColEval {
+    static constexpr int N = 1 << L, NT = NT_;
     uint8_t f[PTS];
     uint32_t vt[PTS];
     __device__ __forceinline__ void load(const ColArgs& a) {
@@ -646,6 +649,320 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
 #endif
 }
 
+
+// ---------------------------------------------------------------------------
+// Radix-2 form of the encode and the half decode for 2^8 .. 2^10 rows
+// (col2_kernel): 2 rows per thread, 2^(L-1) threads -- 8 waves at L = 10, two
+// per SIMD -- instead of 4 rows in 2^(L-2) threads.  The codec's time at
+// 1000:1000 x 1 KiB is the dependency chain of one wave (one per SIMD, 128
+// workgroups on 256 CUs): halving a lane's rows halves the
+// chain, and the second wave of each SIMD issues into the first one's
+// stalls, at the price of one in-wave row-bit swap per layer instead of per
+// two.  A layer's butterfly pairs the thread's two rows (register bit RB);
+// lane bits trade places with RB by DPP / v_permlane swaps (swap2), wave
+// bits by two LDS exchanges around the top layers.  Row-bit maps (RMap<RB,
+// P...>: P_i = the row bit held by thread-index bit i):
+//   S(k)  the IFFT's layer k <= 6: RB = k, lanes b0 .. b6 without b_k,
+//         waves b7 .. (rows 2t, 2t + 1 at S(0): loads and stores contiguous)
+//   M     layers 7 .. L-1: RB = b7, lanes (b0, b1, b2, b3, b8, b9 / b4),
+//         waves the rest (16 consecutive lanes, consecutive rows: the b64
+//         image accesses are conflict-free without a swizzle)
+// ---------------------------------------------------------------------------
+template <int RB, int... P> struct RMap {
+    static constexpr int BITS = sizeof...(P);
+    static __device__ __forceinline__ uint32_t row(uint32_t t, uint32_t m) {
+        uint32_t r = m << RB;
+        int i = 0;
+        ((r |= ((t >> i++) & 1u) << P), ...);
+        return r;
+    }
+};
+// S(k) and M of a 2^L-row column (L = 8 .. 10)
+template <int L, int K> struct SMap;
+#define RS16_S(K, ...)                                                       \
+    template <> struct SMap<8, K> { using M = RMap<K, __VA_ARGS__, 7>; };       \
+    template <> struct SMap<9, K> { using M = RMap<K, __VA_ARGS__, 7, 8>; };    \
+    template <> struct SMap<10, K> { using M = RMap<K, __VA_ARGS__, 7, 8, 9>; };
+RS16_S(0, 1, 2, 3, 4, 5, 6)
+RS16_S(1, 0, 2, 3, 4, 5, 6)
+RS16_S(2, 0, 1, 3, 4, 5, 6)
+RS16_S(3, 0, 1, 2, 4, 5, 6)
+RS16_S(4, 0, 1, 2, 3, 5, 6)
+RS16_S(5, 0, 1, 2, 3, 4, 6)
+RS16_S(6, 0, 1, 2, 3, 4, 5)
+#undef RS16_S
+template <int L> struct MMap;
+template <> struct MMap<8> { using M = RMap<7, 0, 1, 2, 3, 4, 5, 6>; };
+template <> struct MMap<9> { using M = RMap<7, 0, 1, 2, 3, 8, 4, 5, 6>; };
+template <> struct MMap<10> { using M = RMap<7, 0, 1, 2, 3, 8, 9, 4, 5, 6>; };
+// after the swap of lane bit 4 (L >= 9) / 5 (L = 10) in M: the register holds b8 / b9
+template <> struct SMap<9, 8> { using M = RMap<8, 0, 1, 2, 3, 7, 4, 5, 6>; };
+template <> struct SMap<10, 8> { using M = RMap<8, 0, 1, 2, 3, 7, 9, 4, 5, 6>; };
+template <> struct SMap<10, 9> { using M = RMap<9, 0, 1, 2, 3, 7, 8, 4, 5, 6>; };
+template <> struct SMap<8, 7> { using M = RMap<7, 0, 1, 2, 3, 4, 5, 6>; };
+template <> struct SMap<9, 7> { using M = RMap<7, 0, 1, 2, 3, 8, 4, 5, 6>; };
+template <> struct SMap<10, 7> { using M = RMap<7, 0, 1, 2, 3, 8, 9, 4, 5, 6>; };
+
+// Trade the register bit with lane bit LB (rows m = 0, 1; see swap_bit).
+template <int LB> __device__ __forceinline__ void swap2(uint32_t (&X)[2]) {
+    if constexpr (LB == 4 || LB == 5) {
+        const auto r = LB == 4 ? __builtin_amdgcn_permlane16_swap(X[0], X[1], false, false)
+                               : __builtin_amdgcn_permlane32_swap(X[0], X[1], false, false);
+        X[0] = r[0];
+        X[1] = r[1];
+    } else {
+        const bool hi = (threadIdx.x >> LB) & 1u;
+        const uint32_t u = (uint32_t)xshfl<(1 << LB)>((int)X[0]);
+        const uint32_t v = (uint32_t)xshfl<(1 << LB)>((int)X[1]);
+        X[1] = hi ? X[1] : u;
+        X[0] = hi ? v : X[0];
+    }
+}
+template <int LB> __device__ __forceinline__ void swap2(uint32_t (&XL)[2], uint32_t (&XH)[2]) {
+    swap2<LB>(XL);
+    swap2<LB>(XH);
+}
+template <bool FFT> __device__ __forceinline__ void bfly2(uint32_t (&XL)[2], uint32_t (&XH)[2], const uint32_t (&w)[20]) {
+    if (FFT) {
+        mul_xor(XL[0], XH[0], XL[1], XH[1], w);
+        XL[1] ^= XL[0], XH[1] ^= XH[0];
+    } else {
+        XL[1] ^= XL[0], XH[1] ^= XH[0];
+        mul_xor(XL[0], XH[0], XL[1], XH[1], w);
+    }
+}
+// table of layer KB (>= 2: LDS) for the thread's pair under map MP
+template <int L, bool FFT, int KB, class MP>
+__device__ __forceinline__ void tab2(uint32_t (&w)[20], uint32_t t, const uint8_t* smem) {
+    lds_table(w, smem, tab_off<L, FFT>(KB, MP::row(t, 0)));
+}
+// layers 0 and 1 straight from the table image (group index of the image:
+// layer kb at N - 2^(L-kb), row >> (kb + 1))
+template <int L, int KB, class MP>
+__device__ __forceinline__ void tab2_img(uint32_t (&w)[20], uint32_t t, const uint8_t* img) {
+    constexpr uint32_t N = 1u << L;
+    img_table(w, img, (N - (N >> KB)) + (MP::row(t, 0) >> (KB + 1)));
+}
+// rows of map A -> LDS image; barrier; rows of map B <- image
+template <class A, class B>
+__device__ __forceinline__ void exchange2(uint32_t (&XL)[2], uint32_t (&XH)[2], uint32_t t, uint8_t* img8) {
+    uint2* img = (uint2*)img8;
+#pragma unroll
+    for (int m = 0; m < 2; m++) img[A::row(t, m)] = make_uint2(XL[m], XH[m]);
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const uint2 v = img[B::row(t, m)];
+        XL[m] = v.x;
+        XH[m] = v.y;
+    }
+}
+
+template <int L, int MODE>
+__global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
+    static_assert(L >= 8 && L <= 10 && (MODE == COL_ENC || MODE == COL_DEC_EVAL), "radix-2 column codec");
+    constexpr bool DEC = MODE == COL_DEC_EVAL;
+    constexpr int N = 1 << L, NT = N / 2;
+    using S0 = typename SMap<L, 0>::M;
+    using S6 = typename SMap<L, 6>::M;
+    using MM = typename MMap<L>::M;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t t = threadIdx.x;
+    cstamp(a, 0);
+
+    const uint32_t total = a.qrow * a.nstripes;
+    uint32_t g = blockIdx.x;
+    if ((total & 7u) == 0) g = (g & 7u) * (total >> 3) + (g >> 3);
+    const uint32_t st = g / a.qrow, q = g - st * a.qrow;
+    const uint32_t offL = (q >> 3) * 64u + (q & 7u) * 4u;
+    const uint8_t* in = a.in + st * a.bs_in + offL;
+    uint8_t* out = a.out + st * a.bs_out + offL;
+    if (a.flags) a.flags += st * a.bs_flags;
+
+    auto dma_tables = [&]() {
+        constexpr int G0 = ColSmem<L>::G0;
+        dma_copy<NT>(a.img_ifft + G0 * 80, smem + ColSmem<L>::A, (N - 1 - G0) * 80);
+        dma_copy<NT>(a.img_fft + G0 * 80, smem + ColSmem<L>::B, (N - 1 - G0) * 80);
+    };
+    // ---- requests, as col_kernel: the decoder's flags and polynomial
+    // inputs first, then the layer-0/1 tables into registers, the rows, the DMA
+    [[maybe_unused]] uint8_t fr[2] = {0, 0};
+    [[maybe_unused]] ColEval<L, (DEC ? 2 * N / NT : 1), NT> ce;
+    if constexpr (DEC) {
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const uint32_t r = S0::row(t, m);
+            const uint8_t* fp = r < a.in_rows && a.flags ? a.flags + r : a.zero;
+            fr[m] = *(const __attribute__((address_space(1))) uint8_t*)fp;
+        }
+        ce.load(a);
+    }
+    // (the FFT's layer-0/1 tables are requested after the prologue, under
+    // the IFFT: the prologue is bound by the CU's L2 bandwidth, and a thread's
+    // own tables for layers 0 and 1 are most of its bytes)
+    uint32_t i0[20], i1[20], f0[20], f1[20];
+    tab2_img<L, 0, S0>(i0, t, a.img_ifft);
+    tab2_img<L, 1, typename SMap<L, 1>::M>(i1, t, a.img_ifft);
+    uint32_t XL[2], XH[2];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const uint32_t r = S0::row(t, m);
+        const uint8_t* src = a.zero + (offL & 0x7FFFu);
+        if (r < a.in_rows) src = in + (size_t)r * a.S_in;
+        const uint32_t* p = (const uint32_t*)src;
+        XL[m] = p[0];
+        XH[m] = p[8];
+    }
+    if constexpr (!DEC) dma_tables();
+    [[maybe_unused]] uint32_t ev[2] = {0, 0};
+    if constexpr (DEC) {
+        uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
+        ce.prep(a);
+        ce.run(a, elds);
+        __syncthreads();
+        uint32_t gt[2][20];
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const uint32_t r = S0::row(t, m);
+            const bool rcv = r < a.in_rows && (!a.flags || fr[m] != 0);
+            glb_table(gt[m], a.mul_tab, rcv ? elds[a.base_in + r] : ZERO_ENTRY);
+            ev[m] = elds[a.base_out + r];
+        }
+        dma_tables();
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            uint32_t zl = 0, zh = 0;
+            mul_xor(zl, zh, XL[m], XH[m], gt[m]);
+            XL[m] = zl;
+            XH[m] = zh;
+        }
+    }
+    cstamp(a, 1);
+    // ---- IFFT layers 0 .. 6 in registers and lanes
+    bfly2<false>(XL, XH, i0);
+    __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
+    __syncthreads();
+    cstamp(a, 2);
+    tab2_img<L, 0, S0>(f0, t, a.img_fft);
+    tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, a.img_fft);
+    // Each layer's LDS table is read one layer ahead (wa / wb), so its
+    // latency hides under the previous layer's swap and butterfly.
+    uint8_t* img = smem + ColSmem<L>::IMG;
+    uint32_t wa[20], wb[20];
+    using S2 = typename SMap<L, 2>::M;
+    using S3 = typename SMap<L, 3>::M;
+    using S4 = typename SMap<L, 4>::M;
+    using S5 = typename SMap<L, 5>::M;
+    tab2<L, false, 2, S2>(wa, t, smem);
+    swap2<0>(XL, XH);
+    bfly2<false>(XL, XH, i1);
+    tab2<L, false, 3, S3>(wb, t, smem);
+    swap2<1>(XL, XH);
+    bfly2<false>(XL, XH, wa);
+    tab2<L, false, 4, S4>(wa, t, smem);
+    swap2<2>(XL, XH);
+    bfly2<false>(XL, XH, wb);
+    tab2<L, false, 5, S5>(wb, t, smem);
+    swap2<3>(XL, XH);
+    bfly2<false>(XL, XH, wa);
+    tab2<L, false, 6, S6>(wa, t, smem);
+    swap2<4>(XL, XH);
+    bfly2<false>(XL, XH, wb);
+    tab2<L, false, 7, MM>(wb, t, smem);
+    swap2<5>(XL, XH);
+    bfly2<false>(XL, XH, wa);
+    cstamp(a, 3);
+    // ---- layers 7 .. L-1 both ways around the middle, map M
+    if constexpr (L == 10) {
+        using S8 = typename SMap<L, 8>::M;
+        using S9 = typename SMap<L, 9>::M;
+        tab2<L, false, 8, S8>(wa, t, smem);
+        exchange2<S6, MM>(XL, XH, t, img);
+        bfly2<false>(XL, XH, wb);  // IFFT 7
+        tab2<L, false, 9, S9>(wb, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<false>(XL, XH, wa);  // IFFT 8
+        tab2<L, true, 9, S9>(wa, t, smem);
+        swap2<5>(XL, XH);
+        bfly2<false>(XL, XH, wb);  // IFFT 9
+        tab2<L, true, 8, S8>(wb, t, smem);
+        bfly2<true>(XL, XH, wa);   // FFT 9
+        tab2<L, true, 7, MM>(wa, t, smem);
+        swap2<5>(XL, XH);
+        bfly2<true>(XL, XH, wb);   // FFT 8
+        tab2<L, true, 6, S6>(wb, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<true>(XL, XH, wa);   // FFT 7
+    } else if constexpr (L == 9) {
+        using S8 = typename SMap<L, 8>::M;
+        tab2<L, false, 8, S8>(wa, t, smem);
+        exchange2<S6, MM>(XL, XH, t, img);
+        bfly2<false>(XL, XH, wb);  // IFFT 7
+        tab2<L, true, 8, S8>(wb, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<false>(XL, XH, wa);  // IFFT 8
+        tab2<L, true, 7, MM>(wa, t, smem);
+        bfly2<true>(XL, XH, wb);   // FFT 8
+        tab2<L, true, 6, S6>(wb, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<true>(XL, XH, wa);   // FFT 7
+    } else {
+        tab2<L, true, 7, MM>(wa, t, smem);
+        exchange2<S6, MM>(XL, XH, t, img);
+        bfly2<false>(XL, XH, wb);  // IFFT 7
+        tab2<L, true, 6, S6>(wb, t, smem);
+        bfly2<true>(XL, XH, wa);   // FFT 7
+    }
+    cstamp(a, 4);
+    tab2<L, true, 5, S5>(wa, t, smem);
+    // (each thread writes the image rows it read in the first exchange: no barrier)
+    exchange2<MM, S6>(XL, XH, t, img);
+    bfly2<true>(XL, XH, wb);  // FFT 6
+    tab2<L, true, 4, S4>(wb, t, smem);
+    swap2<5>(XL, XH);
+    bfly2<true>(XL, XH, wa);
+    tab2<L, true, 3, S3>(wa, t, smem);
+    swap2<4>(XL, XH);
+    bfly2<true>(XL, XH, wb);
+    tab2<L, true, 2, S2>(wb, t, smem);
+    swap2<3>(XL, XH);
+    bfly2<true>(XL, XH, wa);
+    swap2<2>(XL, XH);
+    bfly2<true>(XL, XH, wb);
+    swap2<1>(XL, XH);
+    bfly2<true>(XL, XH, f1);
+    [[maybe_unused]] uint32_t rt[DEC ? 2 : 1][20];
+    if constexpr (DEC) {
+#pragma unroll
+        for (int m = 0; m < 2; m++) glb_table(rt[m], a.mul_tab, GF_MODULUS - ev[m]);
+    }
+    swap2<0>(XL, XH);
+    bfly2<true>(XL, XH, f0);
+    cstamp(a, 9);
+    // ---- store rows < out_rows (DEC: revealed, rate_high.rs:236-242)
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const uint32_t r = S0::row(t, m);
+        uint32_t vl = XL[m], vh = XH[m];
+        if constexpr (DEC) {
+            uint32_t zl = 0, zh = 0;
+            mul_xor(zl, zh, vl, vh, rt[m]);
+            vl = zl;
+            vh = zh;
+        }
+        if (r < a.out_rows) {
+            uint32_t* p = (uint32_t*)(out + (size_t)r * a.S_out);
+            __builtin_nontemporal_store(vl, p);
+            __builtin_nontemporal_store(vh, p + 8);
+        }
+    }
+    cstamp(a, 10);
+#if RS16_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    cstamp(a, 11);
+#endif
+}
+
 }  // namespace
 
 int col_rows_ok(uint32_t L) { return L >= COL_LMIN && L <= COL_LMAX; }
@@ -663,14 +980,24 @@ hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
 #undef RS16_COL_ROW
     static const int lds[6] = {ColSmem<6>::BYTES, ColSmem<7>::BYTES,  ColSmem<8>::BYTES,
                                ColSmem<9>::BYTES, ColSmem<10>::BYTES, ColSmem<11>::BYTES};
-    const ColFn fn = fns[L - COL_LMIN][mode];
+    ColFn fn = fns[L - COL_LMIN][mode];
     if (!fn) return hipErrorInvalidValue;  // (the ework decoder needs 4 waves: L >= 9)
+    uint32_t threads = (1u << L) / 4;
+    // the encode and the half decode of 2^8 .. 2^10 rows: the radix-2 form
+    // (2 rows per thread), unless RS16_DIAG_COL_RADIX4
+    if ((mode == COL_ENC || mode == COL_DEC_EVAL) && L >= 8 && L <= 10 && !(g_diag & DIAG_COL_RADIX4)) {
+        static const ColFn fns2[3][2] = {{col2_kernel<8, COL_ENC>, col2_kernel<8, COL_DEC_EVAL>},
+                                         {col2_kernel<9, COL_ENC>, col2_kernel<9, COL_DEC_EVAL>},
+                                         {col2_kernel<10, COL_ENC>, col2_kernel<10, COL_DEC_EVAL>}};
+        fn = fns2[L - 8][mode == COL_ENC ? 0 : 1];
+        threads = (1u << L) / 2;
+    }
     const int bytes = lds[L - COL_LMIN];
     if (bytes > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3((1u << L) / 4), bytes, s, a);
+    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3(threads), bytes, s, a);
     return hipGetLastError();
 }
 

@@ -24,4 +24,11 @@ for grp in FETCH_SIZE WRITE_SIZE \
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$O/pmc$i" -o run --output-format csv \
       -- python3 "$R/bench.py" $P > "$O/pmc$i.log" 2>&1 || fail pmc$i "$O/pmc$i.log"
 done
+# the same traffic counters over the 1 %-loss general decode and the column
+# codec's 1000:1000 workloads (scripts/pmc_extra.py)
+for grp in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d "$O/pmc$i" -o run --output-format csv \
+      -- python3 "$R/scripts/pmc_extra.py" 5 > "$O/pmc$i.log" 2>&1 || fail pmc$i "$O/pmc$i.log"
+done
 echo PROFILE_DONE

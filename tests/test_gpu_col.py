@@ -37,6 +37,17 @@ def no_column():
     rs16.set_diagnostics(old)
 
 
+@pytest.fixture(params=["radix2", "radix4"])
+def form(request):
+    # the encode / half decode of 2^8 .. 2^10 rows run the radix-2 kernel
+    # (col2_kernel, 2 rows per thread) by default; RS16_DIAG_COL_RADIX4 keeps
+    # the 4-rows-per-thread kernel (col_kernel) for them
+    old = rs16.set_diagnostics(0)  # (keeps the flags other fixtures set)
+    rs16.set_diagnostics(old | (rs16.DIAG_COL_RADIX4 if request.param == "radix4" else 0))
+    yield request.param
+    rs16.set_diagnostics(old)
+
+
 def dev_encode(eng, original, m):
     k, sb = original.shape
     d_orig = DeviceArray.from_numpy(eng, original)
@@ -69,7 +80,7 @@ CASES = [(1, 257), (100, 300), (257, 512), (512, 512), (300, 1000), (1000, 1000)
 
 @pytest.mark.parametrize("k,m", CASES)
 @pytest.mark.parametrize("sb", [64, 1024])
-def test_col_encode_vs_oracle(eng, k, m, sb):
+def test_col_encode_vs_oracle(eng, k, m, sb, form):
     original = generate_original(k, sb, k + 7 * m + sb)
     assert np.array_equal(dev_encode(eng, original, m), O.encode(k, m, original))
 
@@ -103,7 +114,7 @@ def test_col_matches_pass_codec(eng, k, m, no_column):
 @pytest.mark.parametrize("k,m", [(1000, 1000), (512, 512), (257, 300), (100, 1000), (1024, 1024), (600, 1024),
                                  (1000, 520), (100, 100), (60, 64), (200, 256), (33, 64), (128, 200)])
 @pytest.mark.parametrize("lost_rec", [0, 5])
-def test_col_half_decode(eng, k, m, lost_rec):
+def test_col_half_decode(eng, k, m, lost_rec, form):
     """Every original lost, recovery shards given (some of them lost too):
     the half-transform decode; restored bit for bit."""
     if m - lost_rec < k:
@@ -149,7 +160,7 @@ def test_col_rate_api_in_place(eng, rate, k, m):
 
 @pytest.mark.parametrize("k,m,n,sb", [(1000, 1000, 5, 128), (512, 512, 3, 128), (300, 1000, 4, 128),
                                       (1000, 1000, 6, 1024), (100, 100, 7, 192)])
-def test_col_batched_stripes(eng, k, m, n, sb, force_column):
+def test_col_batched_stripes(eng, k, m, n, sb, force_column, form):
     pad = 64
     so, sr = k * sb + pad, m * sb + pad
     stripes = [generate_original(k, sb, 11 * i + k) for i in range(n)]
