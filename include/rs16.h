@@ -417,9 +417,7 @@ enum {
                                       column of a tile at any loss count (default: <= 2048 lost) */
     RS16_DIAG_NO_TILE_LAST = 64,   /* ... always as 8-wave items of 32 quad columns */
     RS16_DIAG_FD_LDS = 128,        /* the general decode's in-tile formal derivative always through LDS */
-    RS16_DIAG_COL_RADIX4 = 256,    /* column codec: 4 rows per thread everywhere (no radix-2 form) */
-    RS16_DIAG_NO_NARROW = 512      /* the general decode's first pass keeps its overflow tiles (no
-                                      narrow tail kernel) */
+    RS16_DIAG_COL_RADIX4 = 256     /* column codec: 4 rows per thread everywhere (no radix-2 form) */
 };
 int rs16_set_diagnostics(int flags);
 

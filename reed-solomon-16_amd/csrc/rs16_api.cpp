@@ -145,7 +145,7 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
 extern "C" int rs16_set_diagnostics(int flags) {
     const int old = g_diag;
     g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN |
-                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4 | DIAG_NO_NARROW);
+                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4);
     return old;
 }
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
@@ -153,7 +153,7 @@ extern "C" const char* rs16_prog_name(int prog) {
     static const char* names[] = {"GEN_FFT",   "GEN_IFFT",   "ENC_FIRST",     "ENC_MID",
                                   "ENC_LAST",  "ENC_SINGLE", "DEC_FIRST",     "DEC_MID",
                                   "DEC_LAST",  "DEC_SINGLE", "DEC_HALF_LAST", "DEC_HALF_SINGLE",
-                                  "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY", "COL_ENC", "COL_DEC", "DEC_FIRST_TAIL"};
+                                  "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY", "COL_ENC", "COL_DEC"};
     static_assert(sizeof names / sizeof names[0] == NUM_PROF, "profiling names");
     return (prog >= 0 && prog < NUM_PROF) ? names[prog] : "?";
 }
@@ -239,8 +239,6 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
     };
     if ((he = hipSetDevice(device)) != hipSuccess) return fail(he);
     if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return fail(he);
-    if ((he = hipDeviceGetAttribute(&e->num_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
-        return fail(he);
     if ((he = hipMalloc(&e->d_skew_tab, (size_t)GF_ORDER * TAB_DWORDS * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_mul_tab, t.mul_tab.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_log_walsh, GF_ORDER * 2)) != hipSuccess) return fail(he);

@@ -653,30 +653,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.tile_base = t0z;
     a.lo = 0;
     a.out = Z;
-    // Live tiles beyond one dispatch round (two T = 8 workgroups per CU) of
-    // at most 16 tiles go to tile_first_kernel (one wave per quad column),
-    // which runs them right behind the round instead of at a full item's
-    // latency after it; the kernels count live tiles from zflags on the
-    // device.  One stripe (ns == 1) only.
-    a.narrow_lo = a.narrow_hi = 0;
-    if (lo == 8 && ns == 1 && !var_ns && !(g_diag & DIAG_NO_NARROW)) {
-        const uint32_t nslab = (a.qrow + 31) / 32;
-        const uint32_t per_round = (uint32_t)(2 * num_cu) / nslab;
-        if (per_round > 0 && per_round < t1z - t0z) {
-            a.narrow_lo = per_round;
-            a.narrow_hi = std::min(t1z - t0z, per_round + 16);
-        }
-    }
     RS16_PASS(DEC_FIRST, lo, a, batch(t1z - t0z, 0, 0, zs), s);
-    if (a.narrow_hi > a.narrow_lo) {
-        PassArgs b = a;
-        b.ntiles = t1z - t0z;
-        hipEvent_t ev;
-        if (int rc = prof_begin(s, &ev, err)) return rc;
-        RS16_HIP(launch_tile_first(b, s));
-        if (int rc = prof_end(PROF_DEC_FIRST_TAIL, s, ev, err)) return rc;
-    }
-    a.narrow_lo = a.narrow_hi = 0;
     a.tile_base = 0;
     // Only tiles that contain original rows are needed in the last pass,
     // so DEC_MID computes and stores only U rows of those tiles (its tile

@@ -220,8 +220,7 @@ struct rs16_engine {
     // used when the launch has at most col_max_quads quad columns (x
     // stripes); wider launches take the pass codec, whose tiles share each
     // twiddle table over 32 quad columns.
-    uint32_t col_max_quads = 256;
-    int num_cu = 256;  // compute units of the device (the passes' dispatch round)  // (measured: scripts/probe_col.py)
+    uint32_t col_max_quads = 256;  // (measured: scripts/probe_col.py)
     bool col_ok(int L, size_t S, size_t nstripes, bool gen = false) const;  // gen: the general decode (up to 2^11 rows)
     int col(const rs16::ColArgs& a, int L, int mode, hipStream_t s, rs16_error* err);
     int col_tables(hipStream_t s, rs16_error* err);

@@ -78,7 +78,6 @@ enum ProfId : int {
     PROF_EVAL_POLY,
     PROF_COL_ENC,  // one-launch codec (rs16_col.hip): encode
     PROF_COL_DEC,  // one-launch codec: half-transform decode
-    PROF_DEC_FIRST_TAIL,  // the general decode's first pass, narrow form for the overflow tiles
     NUM_PROF
 };
 
@@ -122,10 +121,6 @@ struct PassArgs {
     // rows straddle the decoder's segment boundary, so HBM addresses are an
     // SGPR row base + a 32-bit lane offset (else 64-bit lane offsets).
     uint32_t voff32;
-    // DEC_FIRST (T = 8, one stripe): the live tiles (zflags 0) of live rank
-    // [narrow_lo, narrow_hi) among the launch's tiles are left to
-    // tile_first_kernel (the overflow beyond one dispatch round)
-    uint32_t narrow_lo, narrow_hi;
     uint32_t fd_lds;  // DEC_MID: in-tile formal derivative through LDS only (DIAG_FD_LDS)
     // Decode zero tiles: zflags[t] = 1 when DEC_FIRST tile t holds no received
     // row (then it is all zero after the erasure multiply and is neither
@@ -242,7 +237,6 @@ enum DiagFlags : int {
     DIAG_NO_TILE_LAST = 64,   // ... always as the 8-wave pass (DEC_LAST items)
     DIAG_FD_LDS = 128,        // DEC_MID's in-tile formal derivative always through the LDS image (tile_fd)
     DIAG_COL_RADIX4 = 256,    // column codec: the 4-rows-per-thread form for every transform (col_kernel)
-    DIAG_NO_NARROW = 512,     // the general decode's first pass runs its overflow tiles itself (no tile_first_kernel)
 };
 extern int g_diag;
 
@@ -254,10 +248,6 @@ hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, h
 // tile_last_kernel): `num_tiles` tiles (x stripes, PassArgs::stripe_tiles)
 // from a.tile_base, rows at lo = 0.
 hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s);
-// The general decode's first pass (T = 8) for the live tiles of rank
-// [narrow_lo, narrow_hi) among tiles [tile_base, tile_base + ntiles) (one
-// wave per quad column, tile_first_kernel)
-hipError_t launch_tile_first(const PassArgs& a, hipStream_t s);
 
 // Elementwise / small kernels.
 hipError_t launch_mul(uint8_t* x, size_t bytes, uint32_t entry, const uint32_t* mul_tab, hipStream_t s);

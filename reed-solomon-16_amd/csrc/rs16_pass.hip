@@ -1332,47 +1332,6 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
 #endif
 }
 
-// live tiles (zflags 0) of the launch [tile_base, tile_base + ntiles) below
-// `tile`, and in all; wave-uniform (the tiles of a 65536-row decode: < 256)
-__device__ __forceinline__ uint32_t live_mask4(const PassArgs& a, uint32_t lane) {
-    const uint32_t w = ((cu32p)a.zflags)[lane];  // tiles 4 lane .. 4 lane + 3
-    uint32_t lv = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const uint32_t tt = 4 * lane + b;
-        if (tt >= a.tile_base && tt < a.tile_base + a.ntiles && !((w >> (8 * b)) & 1u)) lv |= 1u << b;
-    }
-    return lv;
-}
-__device__ __forceinline__ bool narrow_applies(const PassArgs& a, uint32_t lv) {
-    uint32_t total = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) total += (uint32_t)__popcll(__ballot((lv >> b) & 1u));
-    return total > a.narrow_lo && total <= a.narrow_hi;
-}
-// the tile of live rank `want` among the launch's live tiles (lv =
-// live_mask4 of the lane), ~0u if there are not that many; wave-uniform
-__device__ __forceinline__ uint32_t live_tile(uint32_t lv, uint32_t lane, uint32_t want) {
-    uint32_t incl = (uint32_t)__popc(lv);
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= (uint32_t)d) incl += v;
-    }
-    const uint32_t excl = incl - (uint32_t)__popc(lv);
-    const uint64_t hit = __ballot(want >= excl && want < incl);
-    if (!hit) return ~0u;
-    uint32_t cand = 0, seen = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        if ((lv >> b) & 1u) {
-            if (seen == want - excl) cand = 4 * lane + b;
-            seen++;
-        }
-    }
-    return uni((uint32_t)__shfl((int)cand, __ffsll((unsigned long long)hit) - 1));
-}
-
 // The pass: workgroup b processes item b of the launch (4 waves per SIMD,
 // except the one-pass decoders, whose larger register sets take 1).
 template <int P, int T>
@@ -1392,21 +1351,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
 
     uint32_t tile, slab;
     set_item(c, a, item, G::Q, tile, slab);
-    [[maybe_unused]] bool live_order = false;
-    if constexpr (P == DEC_FIRST) {
-        // narrow_hi > narrow_lo (one stripe, T = 8): workgroups take the live
-        // tiles in live-rank order (set_item's tile index = the rank), so the
-        // live items fill the XCDs' slots evenly and the empty workgroups
-        // come last; the ranks [narrow_lo, narrow_hi) are tile_first_kernel's
-        // when the overflow fits it
-        if (a.narrow_hi > a.narrow_lo) {
-            live_order = true;
-            const uint32_t lv = live_mask4(a, c.lane);
-            if (narrow_applies(a, lv) && tile >= a.narrow_lo && tile < a.narrow_hi) return;
-            tile = live_tile(lv, c.lane, tile);
-            if (tile == ~0u) return;
-        }
-    }
+
     if (a.stripe_tiles) {
         // batched stripes: the stripe's arrays, the tile within the stripe
         const uint32_t st = uni(tile / a.stripe_tiles);
@@ -1427,7 +1372,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
         if (a.zflags) a.zflags += st * a.bs_zflags;
         if (a.lostrange) a.lostrange += st * a.bs_lost;
     }
-    if (!live_order) tile += a.tile_base;
+    tile += a.tile_base;
     c.b_low = tile & ((1u << a.lo) - 1);
     c.b_high = tile >> a.lo;
     if constexpr (P == DEC_FIRST) {
@@ -1654,139 +1599,6 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
         __builtin_nontemporal_store(ol, p);
         __builtin_nontemporal_store(oh, p + 8);
     }
-}
-
-// ---------------------------------------------------------------------------
-// The general decode's first pass for the overflow tiles (DEC_FIRST, T = 8:
-// gather received rows x erasure multiplier -> IFFT of the tile's 8 low row
-// bits -> store, rate_high.rs:203-232).  A decode whose received rows lie in
-// slightly more live tiles than one dispatch round holds (the reference
-// bench's 1 % loss: 129 live tiles x 4 slabs = 516 items on 512 slots) used to
-// run the few extra items alone after the round, at an item's full latency
-// (15 us).  The pass leaves the live tiles of rank [narrow_lo, narrow_hi) to
-// this kernel, which runs them one wave per quad column (4 rows per lane, the
-// column codec's radix-4 blocks; a quarter of an item's chain) right behind
-// the round.  Both kernels see the same zflags, so they agree on the ranks;
-// when the overflow exceeds narrow_hi - narrow_lo, neither splits and the
-// pass runs every tile itself.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) tile_first_kernel(PassArgs a) {
-    using namespace colops;
-    constexpr int T = 8;
-    constexpr uint32_t NTAB = (1u << T) - 1;
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[NTAB * 80];
-    __shared__ uint32_t elds[256];
-    const uint32_t t = threadIdx.x, lane = t & 63, w = uni(t >> 6);
-    const uint32_t nq4 = (a.qrow + 3) / 4;
-    const uint32_t k = blockIdx.x / nq4, qg = blockIdx.x - k * nq4;
-    // ---- the tile of live rank narrow_lo + k (uniform)
-    const uint32_t lv = live_mask4(a, lane);
-    if (!narrow_applies(a, lv)) return;
-    const uint32_t tile = live_tile(lv, lane, a.narrow_lo + k);
-    if (tile == ~0u) return;
-    const uint32_t q = qg * 4 + w;
-    const bool active = q < a.qrow;
-    const uint32_t offL = (q >> 3) * 64 + (q & 7) * 4;
-    const uint32_t row0 = (tile << T) + a.row_base_in;  // gather-space row of the tile's row 0
-    // ---- requests: erasure-log block (wave 0, eval_poly's last H_lo left
-    // to this pass), received bits and rows (rows 4 lane + m: block (0, 1)),
-    // then the tile's IFFT twiddles by LDS-DMA
-    uint32_t ev[4] = {0, 0, 0, 0};
-    if (a.ework && w == 0) {
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) ev[jj] = a.ework[(row0 & ~255u) + lane + 64u * jj];
-    }
-    const uint32_t rbw = a.rbits[(row0 + 4 * lane) >> 5] >> ((row0 + 4 * lane) & 31);
-    uint32_t XL[4], XH[4];
-    const uint8_t* zpage = a.zero + (offL & 0x7FFFu);
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        const uint32_t r = row0 + 4 * lane + m;
-        const uint8_t* src = zpage;
-        if (active && ((rbw >> m) & 1u))
-            src = (r >= a.chunk ? a.seg_b + (uint64_t)(r - a.chunk) * a.S_seg : a.seg_a + (uint64_t)r * a.S_seg) + offL;
-        XL[m] = ((const uint32_t*)src)[0];
-        XH[m] = ((const uint32_t*)src)[8];
-    }
-#pragma unroll
-    for (uint32_t i = 0; i * 256 < NTAB * 5; i++) {
-        const uint32_t c = i * 256 + t;
-        if (c < NTAB * 5) {
-            const uint32_t tb = c / 5, part = c - tb * 5;
-            const uint32_t kb = (uint32_t)(T - 32 + __clz(NTAB - tb));
-            const uint32_t jg = tb - ((1u << T) - (1u << (T - kb)));
-            const uint32_t idx = (tile << T) + (jg << (kb + 1)) + (1u << kb) + a.skew_ifft - 1;
-            __builtin_amdgcn_global_load_lds((colops::glb_vp)(a.skew_tab + (size_t)idx * TAB_DWORDS + part * 4),
-                                             (colops::lds_vp)(tabs + (i * 256 + 64 * w) * 16), 16, 0, 0);
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    if (a.ework && w == 0) {
-        fwht256_wave(ev);  // src/engine.rs:207-218, the last 256-point FWHT
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) elds[lane + 64 * jj] = ev[jj];
-    }
-    __syncthreads();  // tables and logs in LDS
-    // ---- "MULTIPLY SHARDS" (rate_high.rs:203-228): received rows x their
-    // erasure multiplier, other rows zero
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        const uint32_t r = row0 + 4 * lane + m;
-        const bool rcv = active && ((rbw >> m) & 1u);
-        const uint32_t e = a.ework ? elds[r & 255u] : (rcv ? a.elog[r] : 0u);
-        uint32_t gt[20];
-        glb_table(gt, a.mul_tab, rcv ? e : ZERO_ENTRY);
-        uint32_t zl = 0, zh = 0;
-        mul_xor(zl, zh, XL[m], XH[m], gt);
-        XL[m] = zl;
-        XH[m] = zh;
-    }
-    // ---- IFFT of the tile's 8 row bits, low layers first: blocks (0, 1),
-    // (2, 3), (4, 5), (6, 7)
-    auto tabs_of = [&](BlockTabs& bt, auto b0c, auto b1c) {
-        constexpr int B0 = decltype(b0c)::value, B1 = decltype(b1c)::value;
-        const uint32_t r0 = brow<B0, B1>(lane, 0), r2 = brow<B0, B1>(lane, 2);
-        auto off = [](int kb, uint32_t r) { return (((1u << T) - (1u << (T - kb))) + (r >> (kb + 1))) * 80u; };
-        lds_table(bt.w0, tabs, off(B0, r0));
-        lds_table(bt.w2, tabs, off(B0, r2));
-        lds_table(bt.w1, tabs, off(B1, r0));
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    using I4 = std::integral_constant<int, 4>;
-    using I5 = std::integral_constant<int, 5>;
-    using I6 = std::integral_constant<int, 6>;
-    using I7 = std::integral_constant<int, 7>;
-    BlockTabs ta, tb;
-    tabs_of(ta, I0(), I1());
-    tabs_of(tb, I2(), I3());
-    compute<false, true, true>(XL, XH, ta);
-    wave_exchange<0, 1>(XL, XH);
-    tabs_of(ta, I4(), I5());
-    compute<false, true, true>(XL, XH, tb);
-    wave_exchange<2, 3>(XL, XH);
-    tabs_of(tb, I6(), I7());
-    compute<false, true, true>(XL, XH, ta);
-    wave_exchange<4, 5>(XL, XH);
-    compute<false, true, true>(XL, XH, tb);
-    // ---- store the tile's rows (block (6, 7): row lane + 64 m) to Z
-    if (active) {
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            uint32_t* p = (uint32_t*)(a.out + ((uint64_t)(tile << T) + lane + 64u * m) * a.S_out + offL);
-            p[0] = XL[m];
-            p[8] = XH[m];
-        }
-    }
-}
-
-hipError_t launch_tile_first(const PassArgs& a, hipStream_t s) {
-    if (a.narrow_hi <= a.narrow_lo || a.qrow == 0) return hipSuccess;
-    const uint32_t nwg = (a.narrow_hi - a.narrow_lo) * ((a.qrow + 3) / 4);
-    hipLaunchKernelGGL(tile_first_kernel, dim3(nwg), dim3(256), 0, s, a);
-    return hipGetLastError();
 }
 
 hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s) {

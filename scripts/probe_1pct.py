@@ -44,7 +44,7 @@ eng.set_profiling(False)
 print("1 % decode per pass (us):", {n: round(ms * 1e3 / max(c, 1), 2) for n, (ms, c) in prof.items() if c})
 
 # the last pass in both forms (identical results)
-for name, flag in (("default", 0), ("no_narrow", rs16.DIAG_NO_NARROW), ("fd_lds", rs16.DIAG_FD_LDS), ("items", rs16.DIAG_NO_TILE_LAST)):
+for name, flag in (("default", 0), ("fd_lds", rs16.DIAG_FD_LDS), ("items", rs16.DIAG_NO_TILE_LAST)):
     old = rs16.set_diagnostics(flag)
     x.upload(o1)
     eng.set_profiling(True)

@@ -325,40 +325,3 @@ def test_decode_split_formal_derivative(eng, k, m, sb, diag, lost, fd):
         assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
     finally:
         rs16.set_diagnostics(old)
-
-
-def _narrow_masks(k, m, pattern):
-    """Loss patterns whose live DEC_FIRST tiles (256-row tiles of the 65536
-    work rows holding a received row) slightly exceed one dispatch round."""
-    om = np.ones(k, bool)
-    if pattern == "1pct":          # 129 live tiles (benches/benchmarks.rs:84-87)
-        om[k - 327:] = False
-    elif pattern == "every8_4096":  # every B tile live + recovery tiles 0..15: 144
-        om[np.arange(4096) * 8] = False
-    elif pattern == "every8_4352":  # 145 live tiles: beyond the tail kernel's 16
-        om[np.arange(4352) * 7] = False
-    elif pattern == "few":         # 2 lost: 129 live tiles, one recovery tile
-        om[[5, 40000 - 32768]] = False
-    lost = int((~om).sum())
-    rm = np.zeros(m, bool)
-    rm[:lost] = True
-    return om, rm
-
-
-@pytest.mark.parametrize("narrow", [True, False])
-@pytest.mark.parametrize("sb,pattern", [(1024, "1pct"), (1024, "every8_4096"), (1024, "every8_4352"),
-                                        (1024, "few"), (2048, "1pct"), (192, "1pct"), (960, "every8_4096")])
-def test_decode_first_pass_narrow_tail(eng, sb, pattern, narrow):
-    # The general decode's first pass leaves live tiles past one dispatch
-    # round (up to 16) to tile_first_kernel (rs16_pass.hip); RS16_DIAG_NO_NARROW
-    # keeps them in the pass.  Bit-exact restoration either way, over
-    # overflows of 1, 16 and 17 tiles and shard widths with 1..8 slabs.
-    k = m = 32768
-    original = generate_original(k, sb, 23)
-    recovery = dev_encode(eng, original, m)
-    om, rm = _narrow_masks(k, m, pattern)
-    old = rs16.set_diagnostics(0 if narrow else rs16.DIAG_NO_NARROW)
-    try:
-        assert np.array_equal(dev_decode(eng, original, recovery, om, rm), original)
-    finally:
-        rs16.set_diagnostics(old)
