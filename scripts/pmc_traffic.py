@@ -1,61 +1,59 @@
-"""rocprofv3 --pmc CSVs (a FETCH_SIZE pass and a WRITE_SIZE pass of the same
-bench command) -> profiles/pmc_traffic.json: HBM-side bytes per launch of each
-pass program, keyed "<PROG>:<k>:<m>:<S>" as bench.py reads it.
-
-Units and gfx950 correction (/opt/skills/guides/MI355X_MICROARCH.md §HBM,
-cdna_hip_programming.md §7): FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE
-reports 1/2 of the bytes of a coalesced streaming read on gfx950, so
-hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Counters are summed over
-XCD/SE instances per dispatch, then averaged over dispatches.
-
-usage: pmc_traffic.py K M S OUT.json FETCH_DIR WRITE_DIR
-"""
+"""profiles/pmc_traffic.json from a scripts/gpu_profile.sh run: HBM bytes
+per launch of every kernel from its FETCH_SIZE / WRITE_SIZE passes
+(MI355X_MICROARCH.md's rocprofv3 recipe: separate --pmc passes; on gfx950
+FETCH_SIZE counts half of the streamed read bytes, so bytes = (2 FETCH_SIZE +
+WRITE_SIZE) KiB), next to the algorithmic bytes of the launch.
+usage: pmc_traffic.py <prof dir> <tag>"""
 import collections
 import csv
-import glob
 import json
 import re
 import sys
+from pathlib import Path
 
-PROGS = ["GEN_FFT", "GEN_IFFT", "ENC_FIRST", "ENC_MID", "ENC_LAST", "ENC_SINGLE", "DEC_FIRST", "DEC_MID", "DEC_LAST",
-         "DEC_SINGLE", "DEC_HALF_LAST", "DEC_HALF_SINGLE"]
-# The half-transform decode of the 32768:32768 bench reuses two kernels under
-# its own profiling names: pass_kernel<ENC_MID, 8> (same bytes as the
-# encode's) and pass_kernel<DEC_FIRST, 7> (the full decode's DEC_FIRST is T = 8).
-ALIASES = {(3, 8): ["ENC_MID", "DEC_HALF_MID"], (6, 7): ["DEC_HALF_FIRST"]}
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from pmc_summary import short  # noqa: E402
 
-
-def per_launch(d, counter):
-    acc = collections.defaultdict(lambda: collections.defaultdict(float))
-    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            m = re.search(r"pass_kernel<(\d+), (\d+)>", r["Kernel_Name"])
-            if not m:
-                continue
-            key = (int(m.group(1)), int(m.group(2)))
-            for name in ALIASES.get(key, [PROGS[key[0]]]):
-                acc[name][r["Dispatch_Id"]] += float(r["Counter_Value"])
-    return {p: sum(v.values()) / len(v) for p, v in acc.items() if v}
+MB1K = 1024
+# pmc passes of gpu_profile.sh: 1 / 2 = the bench step (32768:32768 x 1 KiB,
+# encode + 100 %-loss decode), 5 / 6 = scripts/pmc_extra.py
+WORK = {
+    "bench": "32768:32768:1024",
+    "extra": {"DEC_FIRST/T8": "32768:32768:1024 1% loss", "DEC_MID/T8": "32768:32768:1024 1% loss",
+              "rs16::tile_last_kernel": "32768:32768:1024 1% loss",
+              "col2_kernel<L10,ENC>": "1000:1000:1024 encode",
+              "col2_kernel<L10,DEC_EVAL>": "1000:1000:1024 100% loss",
+              "col_kernel<L11,DEC_GEN>": "1000:1000:1024 1% loss"},
+}
+def mean_counter(path, counter):
+    acc, ids = collections.defaultdict(float), collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        k = short(r["Kernel_Name"])
+        acc[k] += float(r["Counter_Value"])
+        ids[k].add(r["Dispatch_Id"])
+    return {k: acc[k] / len(ids[k]) for k in acc}
 
 
 def main():
-    k, m, s, out, fdir, wdir = sys.argv[1:7]
-    fetch, write = per_launch(fdir, "FETCH_SIZE"), per_launch(wdir, "WRITE_SIZE")
-    res = {}
-    try:
-        res = json.load(open(out))
-    except (OSError, ValueError):
-        pass
-    for p in sorted(set(fetch) & set(write)):
-        res[f"{p}:{k}:{m}:{s}"] = {
-            "fetch_size_kib": round(fetch[p], 1), "write_size_kib": round(write[p], 1),
-            "hbm_bytes_per_launch": round((2 * fetch[p] + write[p]) * 1024),
-            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE = 1/2 of streamed read bytes)"}
-    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
-    for key, v in res.items():
-        print(key, v["hbm_bytes_per_launch"])
+    d, tag = Path(sys.argv[1]), sys.argv[2]
+    out = {}
+    for fp, wp, extra in ((1, 2, False), (5, 6, True)):
+        f = mean_counter(d / f"pmc{fp}" / "run_counter_collection.csv", "FETCH_SIZE")
+        w = mean_counter(d / f"pmc{wp}" / "run_counter_collection.csv", "WRITE_SIZE")
+        for k in f:
+            if "rocclr" in k or not k:
+                continue
+            if extra and k not in WORK["extra"]:
+                continue  # (the extra run's bench-shaped passes are the bench's)
+            wl = WORK["extra"][k] if extra else WORK["bench"]
+            rec = {"fetch_size_kib": round(f[k], 1), "write_size_kib": round(w.get(k, 0.0), 1),
+                   "hbm_bytes_per_launch": int((2 * f[k] + w.get(k, 0.0)) * MB1K),
+                   "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE = 1/2 of streamed read bytes)",
+                   "workload": wl, "collected": tag}
+            out[f"{k}:{wl}"] = rec
+    print(json.dumps(out, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
