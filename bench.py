@@ -470,11 +470,16 @@ def main():
     # steps and the timed loop, so that the timed loop runs unprofiled and
     # in the state the profiled copy leaves the GPU in (a GPU coming out of
     # idle runs steps ~10-25 of a cold start ~8 % slower while its clocks
-    # settle: extra.sustained).  One column slice, so that
-    # every timed launch is one kernel running alone.
+    # settle: extra.sustained).  Its own first 40 steps warm
+    # the clocks and are not counted.  One column slice, so that every
+    # timed launch is one kernel running alone.
     eng.set_slices(1)
-    eng.profile_reset()
     eng.set_profiling(True)
+    for _ in range(40):
+        step()
+    eng.synchronize()
+    eng.profile()
+    eng.profile_reset()
     timed(step, args.steps)
     eng.set_profiling(False)
     eng.set_slices(args.slices)

@@ -680,6 +680,7 @@ template <int RB, int... P> struct RMap {
 // S(k) and M of a 2^L-row column (L = 8 .. 10)
 template <int L, int K> struct SMap;
 #define RS16_S(K, ...)                                                       \
+    template <> struct SMap<7, K> { using M = RMap<K, __VA_ARGS__>; };          \
     template <> struct SMap<8, K> { using M = RMap<K, __VA_ARGS__, 7>; };       \
     template <> struct SMap<9, K> { using M = RMap<K, __VA_ARGS__, 7, 8>; };    \
     template <> struct SMap<10, K> { using M = RMap<K, __VA_ARGS__, 7, 8, 9>; };
@@ -963,9 +964,179 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Multi-chunk encodes of 128-row chunks in one launch (colm_kernel): the
+// reference benchmark rows 100:1000 and 1000:100 (README.md:130-131), whose
+// pass form is several launches.  One workgroup per quad column, ONE WAVE PER
+// CHUNK, 2 rows per lane (the radix-2 maps of col2_kernel restricted to the
+// 7 row bits of a chunk: register + 6 lane bits, no LDS exchange):
+//   high rate (HighRateEncoder::encode, rate_high.rs:44-83): wave c takes
+//     originals [128 c, 128 c + 128) (rows >= k zero), IFFT skew 128 (c + 1);
+//     the chunks are XORed through LDS into wave 0, which runs the FFT (skew
+//     0) and stores recovery rows < m;
+//   low rate (LowRateEncoder::encode, rate_low.rs:44-83): every wave takes
+//     the originals (rows >= k zero), IFFT skew 0, then its own recovery
+//     chunk's FFT, skew 128 (c + 1), and stores rows 128 c + r < m.
+// Each wave stages its own twiddles (layers 2-6, 31 tables x 80 B per
+// direction, LDS-DMA from skew_tab) and loads those of layers 0 / 1 straight
+// into registers, so no barrier precedes the transforms.
+// ---------------------------------------------------------------------------
+constexpr uint32_t CM_N = 128, CM_TABS = 31, CM_TAB_BYTES = CM_TABS * 80;
+__device__ __forceinline__ uint32_t cm_idx(uint32_t kb, uint32_t r, uint32_t skew) {
+    return (r & ~((2u << kb) - 1u)) + (1u << kb) + skew - 1u;  // group start + d + skew - 1
+}
+// the 31 tables of layers 2-6 at `skew` into dst (table tb: layer kb at
+// 32 - 2^(7-kb) + group), by the calling wave
+__device__ __forceinline__ void cm_stage(const uint32_t* skew_tab, uint8_t* dst, uint32_t skew, uint32_t lane) {
+#pragma unroll
+    for (uint32_t i = 0; i * 64 < CM_TABS * 5; i++) {
+        const uint32_t c = i * 64 + lane;
+        if (c < CM_TABS * 5) {
+            const uint32_t tb = c / 5, part = c - tb * 5;
+            const uint32_t kb = (uint32_t)__clz(31u - tb) - 25u;  // (tb < 16: 2, < 24: 3, < 28: 4, < 30: 5, 30: 6)
+            const uint32_t j = tb - (32u - (1u << (7u - kb)));
+            const uint32_t idx = cm_idx(kb, j << (kb + 1), skew);
+            __builtin_amdgcn_global_load_lds((glb_vp)(skew_tab + (size_t)idx * TAB_DWORDS + part * 4),
+                                             (lds_vp)(dst + i * 64 * 16), 16, 0, 0);
+        }
+    }
+}
+template <int KB, class MP>
+__device__ __forceinline__ void cm_tab(uint32_t (&w)[20], uint32_t lane, const uint8_t* base) {
+    const uint32_t r = MP::row(lane, 0);
+    lds_table(w, base, (32u - (1u << (7 - KB)) + (r >> (KB + 1))) * 80u);
+}
+
+template <bool HI>
+__global__ __launch_bounds__(1024) void colm_kernel(ColArgs a) {
+    using S0 = typename SMap<7, 0>::M;
+    using S1 = typename SMap<7, 1>::M;
+    using S2 = typename SMap<7, 2>::M;
+    using S3 = typename SMap<7, 3>::M;
+    using S4 = typename SMap<7, 4>::M;
+    using S5 = typename SMap<7, 5>::M;
+    using S6 = typename SMap<7, 6>::M;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t t = threadIdx.x, lane = t & 63, c = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t total = a.qrow * a.nstripes;
+    uint32_t g = blockIdx.x;
+    if ((total & 7u) == 0) g = (g & 7u) * (total >> 3) + (g >> 3);
+    const uint32_t st = g / a.qrow, q = g - st * a.qrow;
+    const uint32_t offL = (q >> 3) * 64u + (q & 7u) * 4u;
+    const uint8_t* in = a.in + st * a.bs_in + offL;
+    uint8_t* out = a.out + st * a.bs_out + offL;
+    const uint32_t sk_i = HI ? (c + 1) * CM_N : 0u, sk_f = HI ? 0u : (c + 1) * CM_N;
+    const bool fft_wave = !HI || c == 0;
+    uint8_t* tI = smem + c * 2 * CM_TAB_BYTES;
+    uint8_t* tF = tI + CM_TAB_BYTES;
+    // ---- requests: layer-0/1 tables, rows, then the LDS-DMA of layers 2-6
+    uint32_t i0[20], i1[20], f0[20], f1[20];
+    glb_table(i0, a.skew_tab, cm_idx(0, S0::row(lane, 0), sk_i));
+    glb_table(i1, a.skew_tab, cm_idx(1, S1::row(lane, 0), sk_i));
+    uint32_t XL[2], XH[2];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const uint32_t r = (HI ? c * CM_N : 0u) + S0::row(lane, m);
+        const uint8_t* src = a.zero + (offL & 0x7FFFu);
+        if (r < a.in_rows) src = in + (size_t)r * a.S_in;
+        XL[m] = ((const uint32_t*)src)[0];
+        XH[m] = ((const uint32_t*)src)[8];
+    }
+    cm_stage(a.skew_tab, tI, sk_i, lane);
+    if (fft_wave) cm_stage(a.skew_tab, tF, sk_f, lane);
+    __builtin_amdgcn_s_waitcnt(0);  // (the wave's own rows and tables: no barrier)
+    if (fft_wave) {  // (needed at the end: requested under the IFFT)
+        glb_table(f0, a.skew_tab, cm_idx(0, S0::row(lane, 0), sk_f));
+        glb_table(f1, a.skew_tab, cm_idx(1, S1::row(lane, 0), sk_f));
+    }
+    // ---- IFFT layers 0 .. 6 (register + lane bits)
+    uint32_t wa[20], wb[20];
+    cm_tab<2, S2>(wa, lane, tI);
+    bfly2<false>(XL, XH, i0);
+    swap2<0>(XL, XH);
+    bfly2<false>(XL, XH, i1);
+    cm_tab<3, S3>(wb, lane, tI);
+    swap2<1>(XL, XH);
+    bfly2<false>(XL, XH, wa);
+    cm_tab<4, S4>(wa, lane, tI);
+    swap2<2>(XL, XH);
+    bfly2<false>(XL, XH, wb);
+    cm_tab<5, S5>(wb, lane, tI);
+    swap2<3>(XL, XH);
+    bfly2<false>(XL, XH, wa);
+    cm_tab<6, S6>(wa, lane, tI);
+    swap2<4>(XL, XH);
+    bfly2<false>(XL, XH, wb);
+    swap2<5>(XL, XH);
+    bfly2<false>(XL, XH, wa);
+    if constexpr (HI) {
+        // ---- XOR of the chunks' IFFTs (rate_high.rs:55-75) into wave 0
+        uint2* img = (uint2*)(smem + a.nch * 2 * CM_TAB_BYTES);
+        if (c != 0) {
+#pragma unroll
+            for (int m = 0; m < 2; m++) img[c * CM_N + S6::row(lane, m)] = make_uint2(XL[m], XH[m]);
+        }
+        __syncthreads();
+        if (c != 0) return;
+        for (uint32_t cc = 1; cc < a.nch; cc++) {
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                const uint2 v = img[cc * CM_N + S6::row(lane, m)];
+                XL[m] ^= v.x;
+                XH[m] ^= v.y;
+            }
+        }
+    }
+    // ---- FFT layers 6 .. 0
+    cm_tab<6, S6>(wa, lane, tF);
+    cm_tab<5, S5>(wb, lane, tF);
+    bfly2<true>(XL, XH, wa);
+    cm_tab<4, S4>(wa, lane, tF);
+    swap2<5>(XL, XH);
+    bfly2<true>(XL, XH, wb);
+    cm_tab<3, S3>(wb, lane, tF);
+    swap2<4>(XL, XH);
+    bfly2<true>(XL, XH, wa);
+    cm_tab<2, S2>(wa, lane, tF);
+    swap2<3>(XL, XH);
+    bfly2<true>(XL, XH, wb);
+    swap2<2>(XL, XH);
+    bfly2<true>(XL, XH, wa);
+    swap2<1>(XL, XH);
+    bfly2<true>(XL, XH, f1);
+    swap2<0>(XL, XH);
+    bfly2<true>(XL, XH, f0);
+    // ---- store recovery rows < m
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const uint32_t r = (HI ? 0u : c * CM_N) + S0::row(lane, m);
+        if (r < a.out_rows) {
+            uint32_t* p = (uint32_t*)(out + (size_t)r * a.S_out);
+            __builtin_nontemporal_store(XL[m], p);
+            __builtin_nontemporal_store(XH[m], p + 8);
+        }
+    }
+}
+
 }  // namespace
 
 int col_rows_ok(uint32_t L) { return L >= COL_LMIN && L <= COL_LMAX; }
+
+hipError_t launch_col_multi(const ColArgs& a, bool high, hipStream_t s) {
+    if (a.nch == 0 || a.nch > COLM_MAX_CHUNKS) return hipErrorInvalidValue;
+    if (a.qrow == 0 || a.nstripes == 0 || a.out_rows == 0) return hipSuccess;
+    const int bytes = (int)(a.nch * 2 * CM_TAB_BYTES + (high ? a.nch * CM_N * 8 : 0));
+    const auto fn = high ? colm_kernel<true> : colm_kernel<false>;
+    static bool attr[2] = {false, false};  // (idempotent: a racing second call sets it again)
+    if (!attr[high]) {
+        const int most = (int)(COLM_MAX_CHUNKS * 2 * CM_TAB_BYTES + COLM_MAX_CHUNKS * CM_N * 8);
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, most);
+        if (e != hipSuccess) return e;
+        attr[high] = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3(64 * a.nch), bytes, s, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
     if (L < COL_LMIN || L > COL_LGEN || mode < COL_ENC || mode > COL_DEC_GEN) return hipErrorInvalidValue;

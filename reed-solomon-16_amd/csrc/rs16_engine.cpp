@@ -280,6 +280,24 @@ int rs16_engine::col(const ColArgs& args, int L, int mode, hipStream_t s, rs16_e
     return prof_end(prof, s, ev, err);
 }
 
+// The multi-chunk encodes of 128-row chunks in one launch (colm_kernel,
+// rs16_col.hip): nch chunks of originals (high) or of recovery (low).
+int rs16_engine::col_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec,
+                           uint32_t nch, bool high, hipStream_t s, rs16_error* err) {
+    ColArgs c = col_args();
+    c.in = d_orig;
+    c.out = d_rec;
+    c.S_in = c.S_out = S_user;
+    c.qrow = (uint32_t)(S / 8);
+    c.in_rows = (uint32_t)k;
+    c.out_rows = (uint32_t)m;
+    c.nch = nch;
+    hipEvent_t ev;
+    if (int rc = prof_begin(s, &ev, err)) return rc;
+    RS16_HIP(launch_col_multi(c, high, s));
+    return prof_end(PROF_COL_ENC, s, ev, err);
+}
+
 // Engine::fft over 2^L rows: L <= 8 in one pass; otherwise the high
 // (L - L/2) row bits as a strided pass, then the low L/2 bits contiguous.
 int rs16_engine::fft(uint8_t* data, size_t S, size_t pos, size_t size, size_t skew_delta, hipStream_t s,
@@ -737,6 +755,8 @@ int rs16_engine::encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, 
         if (d_rec != Z) RS16_HIP(hipMemcpyAsync(d_rec, Z, S, hipMemcpyDeviceToDevice, s));
         return RS16_OK;
     }
+    if (L == (int)COLM_L && nch <= COLM_MAX_CHUNKS && col_ok(L, S, 1))
+        return col_multi(k, m, S, S_user, d_orig, d_rec, nch, true, s, err);
     PassArgs a = base_args(this, S);
     a.seg_a = d_orig;
     a.S_seg = S_user;
@@ -784,6 +804,8 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
         c.skew_fft = (uint32_t)chunk;
         return col(c, L, COL_ENC, s, err);
     }
+    if (nch > 1 && L == (int)COLM_L && nch <= COLM_MAX_CHUNKS && col_ok(L, S, 1))
+        return col_multi(k, m, S, S_user, d_orig, d_rec, nch, false, s, err);
     // U belongs to the caller's stream (no engine-wide fallback: two calls
     // on concurrent streams sharing one buffer restored wrong data, round 3)
     if (!U) return set_error(err, RS16_INVALID_ARGUMENT);

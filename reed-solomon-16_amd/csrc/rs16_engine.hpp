@@ -223,6 +223,8 @@ struct rs16_engine {
     uint32_t col_max_quads = 256;  // (measured: scripts/probe_col.py)
     bool col_ok(int L, size_t S, size_t nstripes, bool gen = false) const;  // gen: the general decode (up to 2^11 rows)
     int col(const rs16::ColArgs& a, int L, int mode, hipStream_t s, rs16_error* err);
+    int col_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec, uint32_t nch,
+                  bool high, hipStream_t s, rs16_error* err);
     int col_tables(hipStream_t s, rs16_error* err);
     rs16::ColArgs col_args() const;
     // Multi-chunk encoders (high rate with k > chunk, low rate): every chunk's

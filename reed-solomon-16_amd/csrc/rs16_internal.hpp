@@ -216,6 +216,7 @@ struct ColArgs {
     // bs_flags_o bytes, elog + st bs_elog words (0: shared by all stripes)
     uint64_t bs_flags, bs_flags_o;
     uint32_t bs_elog;
+    uint32_t nch;               // launch_col_multi: chunks of 128 rows (one wave each)
     uint64_t* stamps;           // RS16_STAMPS builds: phase timeline (rs16_engine_set_stamps)
 };
 int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec covers
@@ -223,6 +224,11 @@ int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec cover
 // loss pattern; formal derivative in the kernel), polynomial in the kernel
 enum ColMode : int { COL_ENC = 0, COL_DEC_EWORK, COL_DEC_EVAL, COL_DEC_GEN };
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s);
+// Multi-chunk encodes of 128-row chunks in one launch (colm_kernel): high
+// rate (high = 1: nch chunks of originals, one recovery chunk) or low rate
+// (one chunk of originals, nch recovery chunks); nch <= COLM_MAX_CHUNKS
+constexpr uint32_t COLM_L = 7, COLM_MAX_CHUNKS = 16;
+hipError_t launch_col_multi(const ColArgs& a, bool high, hipStream_t s);
 
 // Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):
 // alternative code paths kept for tests and measurements, never needed for

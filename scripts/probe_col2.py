@@ -18,13 +18,21 @@ from rs16.util import generate_original  # noqa: E402
 
 def run(eng, k, m, S, flag):
     o = generate_original(k, S, 0)
-    a, r, x = DeviceArray.from_numpy(eng, o), DeviceArray(eng, m * S), DeviceArray(eng, k * S)
-    f0 = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
-    f1 = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+    # decode: the first min(k, m) originals lost, recovery 0.. given (100 %
+    # original loss when k <= m; benches/benchmarks.rs:82-87)
+    lost = min(k, m)
+    held = o.copy()
+    held[:lost] = 0
+    a, r, x = DeviceArray.from_numpy(eng, o), DeviceArray(eng, m * S), DeviceArray.from_numpy(eng, held)
+    fo = np.ones(k, np.uint8)
+    fo[:lost] = 0
+    fr = np.zeros(m, np.uint8)
+    fr[:lost] = 1
+    f0, f1 = DeviceArray.from_numpy(eng, fo), DeviceArray.from_numpy(eng, fr)
     old = rs16.set_diagnostics(flag)
     try:
         enc = lambda: rs16.encode_device(k, m, S, a.ptr, r.ptr, engine=eng)
-        dec = lambda: rs16.decode_device(k, m, S, x.ptr, f0.ptr, r.ptr, f1.ptr, 0, m, engine=eng)
+        dec = lambda: rs16.decode_device(k, m, S, x.ptr, f0.ptr, r.ptr, f1.ptr, k - lost, lost, engine=eng)
         enc(); dec(); eng.synchronize()
         ok = bool(np.array_equal(x.download(shape=(k, S)), o))
         res = {"exact": ok}
@@ -53,8 +61,9 @@ def run(eng, k, m, S, flag):
 def main():
     eng = rs16.Engine(0)
     out = {}
-    for k, m in ((1000, 1000), (512, 512), (200, 256), (100, 100)):
-        for name, flag in (("radix2", 0), ("radix4", rs16.DIAG_COL_RADIX4)):
+    for k, m in ((1000, 1000), (512, 512), (200, 256), (100, 100), (1000, 100), (100, 1000)):
+        forms = (("radix2", 0), ("radix4", rs16.DIAG_COL_RADIX4)) if k == m else (("column", 0), ("passes", rs16.DIAG_NO_COLUMN))
+        for name, flag in forms:
             out[f"{k}:{m} {name}"] = run(eng, k, m, 1024, flag)
             print(f"{k}:{m} {name}", json.dumps(out[f"{k}:{m} {name}"]), flush=True)
 

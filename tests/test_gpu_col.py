@@ -295,3 +295,21 @@ def test_col_general_decode_rate_api(eng, rate, k, m):
         got = dict(res.restored_original_iter())
     assert sorted(got) == lost
     assert all(np.array_equal(np.frombuffer(got[i], np.uint8), original[i]) for i in lost)
+
+
+@pytest.mark.parametrize("k,m", [(1000, 100), (129, 100), (2048, 128), (300, 65), (2049, 100),
+                                 (100, 1000), (100, 129), (128, 2048), (65, 300), (100, 2100), (1, 200)])
+@pytest.mark.parametrize("sb", [64, 192, 1024])
+def test_col_multi_chunk_encode(eng, k, m, sb):
+    # multi-chunk encodes of 128-row chunks in one launch (colm_kernel, one
+    # wave per chunk; rate_high.rs:44-83 / rate_low.rs:44-83): 2..16 chunks of
+    # either rate, partial last chunks; 17 chunks take the pass form.  Equal
+    # to the oracle and to the pass codec (RS16_DIAG_NO_COLUMN).
+    original = generate_original(k, sb, 5 * k + m + sb)
+    got = dev_encode(eng, original, m)
+    assert np.array_equal(got, O.encode(k, m, original))
+    old = rs16.set_diagnostics(rs16.DIAG_NO_COLUMN)
+    try:
+        assert np.array_equal(dev_encode(eng, original, m), got)
+    finally:
+        rs16.set_diagnostics(old)
