@@ -576,7 +576,14 @@ struct GroupLoop {
                 H[m2] ^= H[m];
             }
         }
-        pin_rows<Geo<T>::NR>(L, H);
+        // (only the group's own rows: a row of a later group may still be
+        // in flight from HBM, and pinning it here would make the compiler
+        // wait for every row load before the second group of the first layer)
+#pragma unroll
+        for (int j = 0; j < (1 << rb); j++) {
+            const int m = (gi << (rb + 1)) + j, m2 = m + (1 << rb);
+            asm volatile("" : "+v"(L[m]), "+v"(H[m]), "+v"(L[m2]), "+v"(H[m2]));
+        }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (S::DF && kb == 0) fin(L, H, gi << 1);  // rows 2 gi, 2 gi + 1 are final
         if constexpr (more)
