@@ -680,6 +680,7 @@ template <int RB, int... P> struct RMap {
 // S(k) and M of a 2^L-row column (L = 8 .. 10)
 template <int L, int K> struct SMap;
 #define RS16_S(K, ...)                                                       \
+    template <> struct SMap<11, K> { using M = RMap<K, __VA_ARGS__, 7, 8, 9, 10>; }; \
     template <> struct SMap<7, K> { using M = RMap<K, __VA_ARGS__>; };          \
     template <> struct SMap<8, K> { using M = RMap<K, __VA_ARGS__, 7>; };       \
     template <> struct SMap<9, K> { using M = RMap<K, __VA_ARGS__, 7, 8>; };    \
@@ -696,6 +697,12 @@ template <int L> struct MMap;
 template <> struct MMap<8> { using M = RMap<7, 0, 1, 2, 3, 4, 5, 6>; };
 template <> struct MMap<9> { using M = RMap<7, 0, 1, 2, 3, 8, 4, 5, 6>; };
 template <> struct MMap<10> { using M = RMap<7, 0, 1, 2, 3, 8, 9, 4, 5, 6>; };
+// L = 11: lanes (b0, b1, b2, b8, b9, b10), waves (b3, b4, b5, b6); lane bits
+// 3 / 4 / 5 then hold b8 / b9 / b10 for the in-wave swaps of the middle
+template <> struct MMap<11> { using M = RMap<7, 0, 1, 2, 8, 9, 10, 3, 4, 5, 6>; };
+template <> struct SMap<11, 8> { using M = RMap<8, 0, 1, 2, 7, 9, 10, 3, 4, 5, 6>; };
+template <> struct SMap<11, 9> { using M = RMap<9, 0, 1, 2, 7, 8, 10, 3, 4, 5, 6>; };
+template <> struct SMap<11, 10> { using M = RMap<10, 0, 1, 2, 7, 8, 9, 3, 4, 5, 6>; };
 // after the swap of lane bit 4 (L >= 9) / 5 (L = 10) in M: the register holds b8 / b9
 template <> struct SMap<9, 8> { using M = RMap<8, 0, 1, 2, 3, 7, 4, 5, 6>; };
 template <> struct SMap<10, 8> { using M = RMap<8, 0, 1, 2, 3, 7, 9, 4, 5, 6>; };
@@ -759,10 +766,42 @@ __device__ __forceinline__ void exchange2(uint32_t (&XL)[2], uint32_t (&XH)[2], 
     }
 }
 
+// The formal derivative (closed form, col_fd) of the radix-2 kernel's rows
+// at the middle, where the register holds row bit RB: that term from the
+// register pair, every other bit's from an LDS image of the column.
+template <class MP, int L, int RB>
+__device__ __forceinline__ void col2_fd(uint32_t (&XL)[2], uint32_t (&XH)[2], uint32_t t, uint8_t* img8) {
+    uint2* img = (uint2*)img8;
+    __syncthreads();  // (every wave is past its earlier image reads)
+#pragma unroll
+    for (int m = 0; m < 2; m++) img[MP::row(t, m)] = make_uint2(XL[m], XH[m]);
+    __syncthreads();
+    uint32_t AL[2], AH[2];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const uint32_t j = MP::row(t, m);
+        uint32_t al = XL[m], ah = XH[m];
+        if (m == 0) al ^= XL[1], ah ^= XH[1];
+#pragma unroll
+        for (int b = 0; b < L; b++) {
+            if (b == RB) continue;
+            const uint2 v = img[j | (1u << b)];
+            const bool take = !((j >> b) & 1u);
+            al ^= take ? v.x : 0u;
+            ah ^= take ? v.y : 0u;
+        }
+        AL[m] = al;
+        AH[m] = ah;
+    }
+#pragma unroll
+    for (int m = 0; m < 2; m++) XL[m] = AL[m], XH[m] = AH[m];
+}
+
 template <int L, int MODE>
 __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
-    static_assert(L >= 8 && L <= 10 && (MODE == COL_ENC || MODE == COL_DEC_EVAL), "radix-2 column codec");
-    constexpr bool DEC = MODE == COL_DEC_EVAL;
+    static_assert(L >= 8 && L <= 11 && (L <= 10 || MODE == COL_DEC_GEN) && MODE != COL_DEC_EWORK,
+                  "radix-2 column codec");
+    constexpr bool DEC = MODE != COL_ENC, GEN = MODE == COL_DEC_GEN;
     constexpr int N = 1 << L, NT = N / 2;
     using S0 = typename SMap<L, 0>::M;
     using S6 = typename SMap<L, 6>::M;
@@ -779,21 +818,26 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     const uint8_t* in = a.in + st * a.bs_in + offL;
     uint8_t* out = a.out + st * a.bs_out + offL;
     if (a.flags) a.flags += st * a.bs_flags;
+    if (a.flags_o) a.flags_o += st * a.bs_flags_o;
 
     auto dma_tables = [&]() {
         constexpr int G0 = ColSmem<L>::G0;
         dma_copy<NT>(a.img_ifft + G0 * 80, smem + ColSmem<L>::A, (N - 1 - G0) * 80);
         dma_copy<NT>(a.img_fft + G0 * 80, smem + ColSmem<L>::B, (N - 1 - G0) * 80);
     };
+    // segments of a row (GEN: A = rows [0, in_rows), B = [chunk, chunk + o_rows))
+    auto in_a = [&](uint32_t r) { return r < a.in_rows; };
+    auto in_b = [&](uint32_t r) { return GEN && r >= a.chunk && r - a.chunk < a.o_rows; };
     // ---- requests, as col_kernel: the decoder's flags and polynomial
     // inputs first, then the layer-0/1 tables into registers, the rows, the DMA
     [[maybe_unused]] uint8_t fr[2] = {0, 0};
-    [[maybe_unused]] ColEval<L, (DEC ? 2 * N / NT : 1), NT> ce;
+    [[maybe_unused]] ColEval<L, (DEC ? (GEN ? N : 2 * N) / NT : 1), NT> ce;
     if constexpr (DEC) {
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             const uint32_t r = S0::row(t, m);
-            const uint8_t* fp = r < a.in_rows && a.flags ? a.flags + r : a.zero;
+            const uint8_t* fp = in_a(r) && a.flags ? a.flags + r
+                                                   : (in_b(r) && a.flags_o ? a.flags_o + (r - a.chunk) : a.zero);
             fr[m] = *(const __attribute__((address_space(1))) uint8_t*)fp;
         }
         ce.load(a);
@@ -809,14 +853,27 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     for (int m = 0; m < 2; m++) {
         const uint32_t r = S0::row(t, m);
         const uint8_t* src = a.zero + (offL & 0x7FFFu);
-        if (r < a.in_rows) src = in + (size_t)r * a.S_in;
+        if (in_a(r)) src = in + (size_t)r * a.S_in;
+        if (in_b(r)) src = a.in_b + st * a.bs_in_b + offL + (size_t)(r - a.chunk) * a.S_in;
         const uint32_t* p = (const uint32_t*)src;
         XL[m] = p[0];
         XH[m] = p[8];
     }
     if constexpr (!DEC) dma_tables();
     [[maybe_unused]] uint32_t ev[2] = {0, 0};
+    [[maybe_unused]] bool lost[2] = {false, false};  // (GEN: the row is a lost original)
     if constexpr (DEC) {
+        bool rcv[2];
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const uint32_t r = S0::row(t, m);
+            rcv[m] = in_a(r) && (!a.flags || fr[m] != 0);
+            if (GEN && a.rev_a && in_a(r)) lost[m] = !rcv[m];  // (low rate: originals = segment A)
+            if (in_b(r)) {
+                rcv[m] = !a.flags_o || fr[m] != 0;
+                if (!a.rev_a) lost[m] = !rcv[m];
+            }
+        }
         uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
         ce.prep(a);
         ce.run(a, elds);
@@ -825,8 +882,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             const uint32_t r = S0::row(t, m);
-            const bool rcv = r < a.in_rows && (!a.flags || fr[m] != 0);
-            glb_table(gt[m], a.mul_tab, rcv ? elds[a.base_in + r] : ZERO_ENTRY);
+            glb_table(gt[m], a.mul_tab, rcv[m] ? elds[a.base_in + r] : ZERO_ENTRY);
             ev[m] = elds[a.base_out + r];
         }
         dma_tables();
@@ -844,8 +900,10 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
     __syncthreads();
     cstamp(a, 2);
-    tab2_img<L, 0, S0>(f0, t, a.img_fft);
-    tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, a.img_fft);
+    if constexpr (L <= 10) {
+        tab2_img<L, 0, S0>(f0, t, a.img_fft);
+        tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, a.img_fft);
+    }
     // Each layer's LDS table is read one layer ahead (wa / wb), so its
     // latency hides under the previous layer's swap and butterfly.
     uint8_t* img = smem + ColSmem<L>::IMG;
@@ -873,8 +931,41 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     swap2<5>(XL, XH);
     bfly2<false>(XL, XH, wa);
     cstamp(a, 3);
-    // ---- layers 7 .. L-1 both ways around the middle, map M
-    if constexpr (L == 10) {
+    // ---- layers 7 .. L-1 both ways around the middle, map M (GEN: the
+    // formal derivative between the IFFT's last layer and the FFT's first)
+    if constexpr (L == 11) {
+        using S8 = typename SMap<L, 8>::M;
+        using S9 = typename SMap<L, 9>::M;
+        using S10 = typename SMap<L, 10>::M;
+        tab2<L, false, 8, S8>(wa, t, smem);
+        exchange2<S6, MM>(XL, XH, t, img);
+        bfly2<false>(XL, XH, wb);  // IFFT 7
+        tab2<L, false, 9, S9>(wb, t, smem);
+        swap2<3>(XL, XH);
+        bfly2<false>(XL, XH, wa);  // IFFT 8
+        tab2<L, false, 10, S10>(wa, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<false>(XL, XH, wb);  // IFFT 9
+        tab2<L, true, 10, S10>(wb, t, smem);
+        swap2<5>(XL, XH);
+        bfly2<false>(XL, XH, wa);  // IFFT 10
+        col2_fd<S10, L, 10>(XL, XH, t, img);
+        tab2<L, true, 9, S9>(wa, t, smem);
+        bfly2<true>(XL, XH, wb);   // FFT 10
+        tab2<L, true, 8, S8>(wb, t, smem);
+        swap2<5>(XL, XH);
+        bfly2<true>(XL, XH, wa);   // FFT 9
+        tab2<L, true, 7, MM>(wa, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<true>(XL, XH, wb);   // FFT 8
+        tab2<L, true, 6, S6>(wb, t, smem);
+        swap2<3>(XL, XH);
+        bfly2<true>(XL, XH, wa);   // FFT 7
+        // (at 16 waves the FFT's layer-0/1 tables are requested here: 128 VGPRs)
+        tab2_img<L, 0, S0>(f0, t, a.img_fft);
+        tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, a.img_fft);
+        __syncthreads();  // (every wave has read its derivative terms from the image)
+    } else if constexpr (L == 10) {
         using S8 = typename SMap<L, 8>::M;
         using S9 = typename SMap<L, 9>::M;
         tab2<L, false, 8, S8>(wa, t, smem);
@@ -886,6 +977,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         tab2<L, true, 9, S9>(wa, t, smem);
         swap2<5>(XL, XH);
         bfly2<false>(XL, XH, wb);  // IFFT 9
+        if constexpr (GEN) col2_fd<S9, L, 9>(XL, XH, t, img);
         tab2<L, true, 8, S8>(wb, t, smem);
         bfly2<true>(XL, XH, wa);   // FFT 9
         tab2<L, true, 7, MM>(wa, t, smem);
@@ -894,6 +986,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         tab2<L, true, 6, S6>(wb, t, smem);
         swap2<4>(XL, XH);
         bfly2<true>(XL, XH, wa);   // FFT 7
+        if constexpr (GEN) __syncthreads();
     } else if constexpr (L == 9) {
         using S8 = typename SMap<L, 8>::M;
         tab2<L, false, 8, S8>(wa, t, smem);
@@ -902,21 +995,26 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         tab2<L, true, 8, S8>(wb, t, smem);
         swap2<4>(XL, XH);
         bfly2<false>(XL, XH, wa);  // IFFT 8
+        if constexpr (GEN) col2_fd<S8, L, 8>(XL, XH, t, img);
         tab2<L, true, 7, MM>(wa, t, smem);
         bfly2<true>(XL, XH, wb);   // FFT 8
         tab2<L, true, 6, S6>(wb, t, smem);
         swap2<4>(XL, XH);
         bfly2<true>(XL, XH, wa);   // FFT 7
+        if constexpr (GEN) __syncthreads();
     } else {
         tab2<L, true, 7, MM>(wa, t, smem);
         exchange2<S6, MM>(XL, XH, t, img);
         bfly2<false>(XL, XH, wb);  // IFFT 7
+        if constexpr (GEN) col2_fd<MM, L, 7>(XL, XH, t, img);
         tab2<L, true, 6, S6>(wb, t, smem);
         bfly2<true>(XL, XH, wa);   // FFT 7
+        if constexpr (GEN) __syncthreads();
     }
     cstamp(a, 4);
     tab2<L, true, 5, S5>(wa, t, smem);
-    // (each thread writes the image rows it read in the first exchange: no barrier)
+    // (each thread writes the image rows it read in the first exchange: no
+    // barrier; GEN: the derivative's image reads are behind a barrier above)
     exchange2<MM, S6>(XL, XH, t, img);
     bfly2<true>(XL, XH, wb);  // FFT 6
     tab2<L, true, 4, S4>(wb, t, smem);
@@ -940,7 +1038,8 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     swap2<0>(XL, XH);
     bfly2<true>(XL, XH, f0);
     cstamp(a, 9);
-    // ---- store rows < out_rows (DEC: revealed, rate_high.rs:236-242)
+    // ---- store rows < out_rows (DEC: revealed, rate_high.rs:236-242; GEN:
+    // the lost originals only, restored in place)
 #pragma unroll
     for (int m = 0; m < 2; m++) {
         const uint32_t r = S0::row(t, m);
@@ -951,8 +1050,9 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
             vl = zl;
             vh = zh;
         }
-        if (r < a.out_rows) {
-            uint32_t* p = (uint32_t*)(out + (size_t)r * a.S_out);
+        const bool st_ok = GEN ? lost[m] : r < a.out_rows;
+        if (st_ok) {
+            uint32_t* p = (uint32_t*)(out + (size_t)(GEN && !a.rev_a ? r - a.chunk : r) * a.S_out);
             __builtin_nontemporal_store(vl, p);
             __builtin_nontemporal_store(vh, p + 8);
         }
@@ -1156,11 +1256,13 @@ hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
     uint32_t threads = (1u << L) / 4;
     // the encode and the half decode of 2^8 .. 2^10 rows: the radix-2 form
     // (2 rows per thread), unless RS16_DIAG_COL_RADIX4
-    if ((mode == COL_ENC || mode == COL_DEC_EVAL) && L >= 8 && L <= 10 && !(g_diag & DIAG_COL_RADIX4)) {
-        static const ColFn fns2[3][2] = {{col2_kernel<8, COL_ENC>, col2_kernel<8, COL_DEC_EVAL>},
-                                         {col2_kernel<9, COL_ENC>, col2_kernel<9, COL_DEC_EVAL>},
-                                         {col2_kernel<10, COL_ENC>, col2_kernel<10, COL_DEC_EVAL>}};
-        fn = fns2[L - 8][mode == COL_ENC ? 0 : 1];
+    if (mode != COL_DEC_EWORK && L >= 8 && !(g_diag & DIAG_COL_RADIX4)) {
+        static const ColFn fns2[4][3] = {
+            {col2_kernel<8, COL_ENC>, col2_kernel<8, COL_DEC_EVAL>, col2_kernel<8, COL_DEC_GEN>},
+            {col2_kernel<9, COL_ENC>, col2_kernel<9, COL_DEC_EVAL>, col2_kernel<9, COL_DEC_GEN>},
+            {col2_kernel<10, COL_ENC>, col2_kernel<10, COL_DEC_EVAL>, col2_kernel<10, COL_DEC_GEN>},
+            {nullptr, nullptr, col2_kernel<11, COL_DEC_GEN>}};
+        fn = fns2[L - 8][mode == COL_ENC ? 0 : (mode == COL_DEC_EVAL ? 1 : 2)];
         threads = (1u << L) / 2;
     }
     const int bytes = lds[L - COL_LMIN];

@@ -235,7 +235,7 @@ def test_col_decode_check_counts(eng, k, m):
                                  # low rate (originals = segment A, erasure tail of ones)
                                  (100, 1000), (60, 1000), (200, 700)])
 @pytest.mark.parametrize("pattern", ["1pct", "random", "mixed"])
-def test_col_general_decode(eng, k, m, pattern):
+def test_col_general_decode(eng, k, m, pattern, form):
     """The general decode (any loss pattern) of up to 2048 work rows in one
     launch: polynomial, gather of both segments, IFFT, formal derivative, FFT,
     reveal (rate_high.rs:168-247); every lost original restored bit for bit,
