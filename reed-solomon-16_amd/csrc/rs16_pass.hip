@@ -716,6 +716,40 @@ __device__ __forceinline__ void exchange(uint32_t (&L)[Geo<T>::NR], uint32_t (&H
     }
 }
 
+// DEC_MID's second layout switch when its consumed rows lie in the
+// layout-B register rows [m0, m0 + ND) (fd_few): only those rows go through
+// LDS -- every thread writes ND rows, the threads whose layout-A rows they
+// are read them -- in one round with one barrier, instead of all 2^T rows
+// in two rounds.  The other threads' rows are not consumed (the layout-A
+// FFT layers skip them, the store masks them).
+template <int T, int ND>
+__device__ __forceinline__ void few_switch(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
+                                           uint2* lds, uint32_t m0) {
+    constexpr int Q = Geo<T>::Q, SHB = Geo<T>::SHB, R = Geo<T>::R, NR = Geo<T>::NR;
+    constexpr uint32_t ROWS = (uint32_t)ND << SHB, PLANE = ROWS * Q;
+    uint32_t* img = (uint32_t*)lds;
+    const uint32_t base = m0 << SHB;
+#pragma unroll
+    for (int m = 0; m < NR; m++) {
+        const uint32_t i = (uint32_t)m - m0;  // (uniform)
+        if (i < (uint32_t)ND) {
+            const uint32_t r = c.s + (i << SHB);  // layout B: k = s + (m << SHB)
+            img[r * Q + c.qt] = L[m];
+            img[PLANE + r * Q + c.qt] = H[m];
+        }
+    }
+    __syncthreads();
+    const uint32_t k0 = c.s << R;  // layout A: k = (s << R) + m
+    if (k0 >= base && k0 < base + ROWS) {
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const uint32_t r = k0 - base + (uint32_t)m;
+            L[m] = img[r * Q + c.qt];
+            H[m] = img[PLANE + r * Q + c.qt];
+        }
+    }
+}
+
 // DEC_MID's formal derivative split by row bits (the two-direction pass's
 // layers: IFFT bits [0, R) in layout A, bits [R, T) in layout B, then the
 // FFT back).  With w = the rows after the layout-A IFFT layers, z = M_B(w)
@@ -1286,9 +1320,14 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                 }
                 rs.issue(a, c, el);
             }
-            exchange<T, NQR, true>(L, H, c, lds, [&]() {
-                if constexpr (LateReveal<P, T>::value) rs.commit(a, c, smem);
-            });
+            if constexpr (SPLIT_FD) {
+                if (fd_few) few_switch<T, FD_ND>(L, H, c, lds, fd_m0);
+                else exchange<T, NQR, true>(L, H, c, lds);
+            } else {
+                exchange<T, NQR, true>(L, H, c, lds, [&]() {
+                    if constexpr (LateReveal<P, T>::value) rs.commit(a, c, smem);
+                });
+            }
             stamp(a, 8);
             prio<P, 4, T>();
             in_b = false;
