@@ -412,7 +412,7 @@ enum {
     RS16_DIAG_EVAL_FULL = 4,       /* eval_poly: the full 65536-point form for n <= 2048 */
     RS16_DIAG_NO_COLUMN = 8,       /* 512 / 1024-row transforms through the pass codec instead of
                                       the one-launch column codec */
-    RS16_DIAG_FORCE_COLUMN = 16,   /* ... through the column codec at any shard width / stripe count */
+    RS16_DIAG_FORCE_COLUMN = 16,   /* ... through the column codec at any shard width / stripe count / chunk count */
     RS16_DIAG_TILE_LAST = 32,      /* the general decode's last pass (65536 work rows) one wave per quad
                                       column of a tile at any loss count (default: <= 2048 lost) */
     RS16_DIAG_NO_TILE_LAST = 64,   /* ... always as 8-wave items of 32 quad columns */

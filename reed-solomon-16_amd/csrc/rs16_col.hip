@@ -61,18 +61,20 @@ using namespace colops;
 // the image into registers at the start (load_tabs01_img), so LDS holds
 // layers 2 .. L-1 of both directions only, staged by LDS-DMA (2 (N/4 - 1)
 // x 80 bytes, 40 KiB at L = 10), the row image and the erasure logs:
+//   IMG the row image of the LDS exchanges (N x 8 bytes)
 //   A   the IFFT's tables of groups >= G2 (layer kb at group N - 2^(L-kb),
 //       group j = row >> (kb+1); G2 = 3N/4 = the first group of layer 2)
 //   B   the FFT's, likewise
-//   IMG the row image of the LDS exchanges (N x 8 bytes)
 //   ELOG the decoder's erasure logs / polynomial scratch (2N x 4 bytes)
+// (an encode launches ELOG bytes, the IFFT-only encode B: more workgroups
+// per CU)
 template <int L> struct ColSmem {
     static constexpr int N = 1 << L;
     static constexpr int G0 = N - N / 4;  // first group of layer 2
-    static constexpr int A = 0;
+    static constexpr int IMG = 0;
+    static constexpr int A = IMG + N * 8;
     static constexpr int B = A + (N - 1 - G0) * 80;
-    static constexpr int IMG = B + (N - 1 - G0) * 80;
-    static constexpr int ELOG = IMG + N * 8;
+    static constexpr int ELOG = B + (N - 1 - G0) * 80;
     static constexpr int BYTES = ELOG + 2 * N * 4;
     static_assert(L >= (int)COL_LMIN && L <= (int)COL_LMAX, "the column codec covers 2^6 .. 2^10 rows");
 };
@@ -82,10 +84,10 @@ template <int L> struct ColSmem {
 template <> struct ColSmem<11> {
     static constexpr int N = 2048;
     static constexpr int G0 = N - N / 4;  // first group of layer 2
-    static constexpr int A = 0;
+    static constexpr int IMG = 0;
+    static constexpr int A = IMG + N * 8;
     static constexpr int B = A + (N - 1 - G0) * 80;
-    static constexpr int IMG = B + (N - 1 - G0) * 80;
-    static constexpr int ELOG = IMG + N * 8;
+    static constexpr int ELOG = B + (N - 1 - G0) * 80;
     static constexpr int BYTES = ELOG + N * 4;
 };
 
@@ -801,11 +803,16 @@ template <int L, int MODE>
 __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     static_assert(L >= 8 && L <= 11 && (L <= 10 || MODE == COL_DEC_GEN) && MODE != COL_DEC_EWORK,
                   "radix-2 column codec");
-    constexpr bool DEC = MODE != COL_ENC, GEN = MODE == COL_DEC_GEN;
+    constexpr bool DEC = MODE == COL_DEC_EVAL || MODE == COL_DEC_GEN, GEN = MODE == COL_DEC_GEN;
+    // the high rate's multi-chunk encode in two launches: IFO = the IFFT of
+    // chunk blockIdx.y of originals, stored whole; FFX = the FFT of the XOR
+    // of a.nch such chunks (launch_col, rs16_engine::encode_high_multi)
+    constexpr bool IFO = MODE == COL_ENC_IFFT, FFX = MODE == COL_ENC_FFTX;
     constexpr int N = 1 << L, NT = N / 2;
     using S0 = typename SMap<L, 0>::M;
     using S6 = typename SMap<L, 6>::M;
     using MM = typename MMap<L>::M;
+    using FM = typename SMap<L, L - 1>::M;  // the rows' map between the IFFT's last layer and the FFT's first
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t t = threadIdx.x;
     cstamp(a, 0);
@@ -819,14 +826,33 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     uint8_t* out = a.out + st * a.bs_out + offL;
     if (a.flags) a.flags += st * a.bs_flags;
     if (a.flags_o) a.flags_o += st * a.bs_flags_o;
+    // Multi-chunk encodes (grid row ch = blockIdx.y; images of consecutive
+    // skew deltas are consecutive, HostTables::col_img): ENC = the low rate's
+    // recovery chunk ch (FFT skew (ch + 1) 2^L, rows ch 2^L ..), IFO = the
+    // high rate's chunk ch of originals (IFFT skew (ch + 1) 2^L)
+    const uint32_t ch = blockIdx.y;
+    uint32_t in_rows = a.in_rows, out_rows = a.out_rows;
+    const uint8_t* img_ifft = a.img_ifft;
+    const uint8_t* img_fft = a.img_fft;
+    if constexpr (MODE == COL_ENC) {
+        out += (size_t)ch * N * a.S_out;
+        out_rows -= ch * N;
+        img_fft += (size_t)ch * (N - 1) * 80;
+    }
+    if constexpr (IFO) {
+        in += (size_t)ch * N * a.S_in;
+        in_rows -= ch * N;
+        out += (size_t)ch * N * a.S_out;
+        img_ifft += (size_t)ch * (N - 1) * 80;
+    }
 
     auto dma_tables = [&]() {
         constexpr int G0 = ColSmem<L>::G0;
-        dma_copy<NT>(a.img_ifft + G0 * 80, smem + ColSmem<L>::A, (N - 1 - G0) * 80);
-        dma_copy<NT>(a.img_fft + G0 * 80, smem + ColSmem<L>::B, (N - 1 - G0) * 80);
+        if constexpr (!FFX) dma_copy<NT>(img_ifft + G0 * 80, smem + ColSmem<L>::A, (N - 1 - G0) * 80);
+        if constexpr (!IFO) dma_copy<NT>(img_fft + G0 * 80, smem + ColSmem<L>::B, (N - 1 - G0) * 80);
     };
     // segments of a row (GEN: A = rows [0, in_rows), B = [chunk, chunk + o_rows))
-    auto in_a = [&](uint32_t r) { return r < a.in_rows; };
+    auto in_a = [&](uint32_t r) { return r < in_rows; };
     auto in_b = [&](uint32_t r) { return GEN && r >= a.chunk && r - a.chunk < a.o_rows; };
     // ---- requests, as col_kernel: the decoder's flags and polynomial
     // inputs first, then the layer-0/1 tables into registers, the rows, the DMA
@@ -846,19 +872,48 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     // the IFFT: the prologue is bound by the CU's L2 bandwidth, and a thread's
     // own tables for layers 0 and 1 are most of its bytes)
     uint32_t i0[20], i1[20], f0[20], f1[20];
-    tab2_img<L, 0, S0>(i0, t, a.img_ifft);
-    tab2_img<L, 1, typename SMap<L, 1>::M>(i1, t, a.img_ifft);
-    uint32_t XL[2], XH[2];
-#pragma unroll
-    for (int m = 0; m < 2; m++) {
-        const uint32_t r = S0::row(t, m);
-        const uint8_t* src = a.zero + (offL & 0x7FFFu);
-        if (in_a(r)) src = in + (size_t)r * a.S_in;
-        if (in_b(r)) src = a.in_b + st * a.bs_in_b + offL + (size_t)(r - a.chunk) * a.S_in;
-        const uint32_t* p = (const uint32_t*)src;
-        XL[m] = p[0];
-        XH[m] = p[8];
+    if constexpr (FFX) {
+        tab2_img<L, 0, S0>(f0, t, img_fft);
+        tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, img_fft);
+    } else {
+        tab2_img<L, 0, S0>(i0, t, img_ifft);
+        tab2_img<L, 1, typename SMap<L, 1>::M>(i1, t, img_ifft);
     }
+    uint32_t XL[2], XH[2];
+    if constexpr (FFX) {
+        // the XOR of the nch chunks' rows (rate_high.rs:56-74), in map FM
+#pragma unroll
+        for (int m = 0; m < 2; m++) XL[m] = XH[m] = 0;
+#pragma unroll 4
+        for (uint32_t c = 0; c < a.nch; c++) {
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                const uint32_t* p = (const uint32_t*)(in + ((size_t)c * N + FM::row(t, m)) * a.S_in);
+                XL[m] ^= p[0];
+                XH[m] ^= p[8];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const uint32_t r = S0::row(t, m);
+            const uint8_t* src = a.zero + (offL & 0x7FFFu);
+            if (in_a(r)) src = in + (size_t)r * a.S_in;
+            if (in_b(r)) src = a.in_b + st * a.bs_in_b + offL + (size_t)(r - a.chunk) * a.S_in;
+            const uint32_t* p = (const uint32_t*)src;
+            XL[m] = p[0];
+            XH[m] = p[8];
+        }
+    }
+    // IFO: every row of the chunk, from the map after the IFFT's last layer
+    auto store_mid = [&]() {
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            uint32_t* p = (uint32_t*)(out + (size_t)FM::row(t, m) * a.S_out);
+            __builtin_nontemporal_store(XL[m], p);
+            __builtin_nontemporal_store(XH[m], p + 8);
+        }
+    };
     if constexpr (!DEC) dma_tables();
     [[maybe_unused]] uint32_t ev[2] = {0, 0};
     [[maybe_unused]] bool lost[2] = {false, false};  // (GEN: the row is a lost original)
@@ -895,15 +950,6 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         }
     }
     cstamp(a, 1);
-    // ---- IFFT layers 0 .. 6 in registers and lanes
-    bfly2<false>(XL, XH, i0);
-    __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
-    __syncthreads();
-    cstamp(a, 2);
-    if constexpr (L <= 10) {
-        tab2_img<L, 0, S0>(f0, t, a.img_fft);
-        tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, a.img_fft);
-    }
     // Each layer's LDS table is read one layer ahead (wa / wb), so its
     // latency hides under the previous layer's swap and butterfly.
     uint8_t* img = smem + ColSmem<L>::IMG;
@@ -912,6 +958,19 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     using S3 = typename SMap<L, 3>::M;
     using S4 = typename SMap<L, 4>::M;
     using S5 = typename SMap<L, 5>::M;
+    if constexpr (FFX) {
+        __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
+        __syncthreads();
+    } else {
+    // ---- IFFT layers 0 .. 6 in registers and lanes
+    bfly2<false>(XL, XH, i0);
+    __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
+    __syncthreads();
+    cstamp(a, 2);
+    if constexpr (L <= 10 && !IFO) {
+        tab2_img<L, 0, S0>(f0, t, img_fft);
+        tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, img_fft);
+    }
     tab2<L, false, 2, S2>(wa, t, smem);
     swap2<0>(XL, XH);
     bfly2<false>(XL, XH, i1);
@@ -931,6 +990,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     swap2<5>(XL, XH);
     bfly2<false>(XL, XH, wa);
     cstamp(a, 3);
+    }
     // ---- layers 7 .. L-1 both ways around the middle, map M (GEN: the
     // formal derivative between the IFFT's last layer and the FFT's first)
     if constexpr (L == 11) {
@@ -968,16 +1028,24 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     } else if constexpr (L == 10) {
         using S8 = typename SMap<L, 8>::M;
         using S9 = typename SMap<L, 9>::M;
-        tab2<L, false, 8, S8>(wa, t, smem);
-        exchange2<S6, MM>(XL, XH, t, img);
-        bfly2<false>(XL, XH, wb);  // IFFT 7
-        tab2<L, false, 9, S9>(wb, t, smem);
-        swap2<4>(XL, XH);
-        bfly2<false>(XL, XH, wa);  // IFFT 8
-        tab2<L, true, 9, S9>(wa, t, smem);
-        swap2<5>(XL, XH);
-        bfly2<false>(XL, XH, wb);  // IFFT 9
-        if constexpr (GEN) col2_fd<S9, L, 9>(XL, XH, t, img);
+        if constexpr (!FFX) {
+            tab2<L, false, 8, S8>(wa, t, smem);
+            exchange2<S6, MM>(XL, XH, t, img);
+            bfly2<false>(XL, XH, wb);  // IFFT 7
+            tab2<L, false, 9, S9>(wb, t, smem);
+            swap2<4>(XL, XH);
+            bfly2<false>(XL, XH, wa);  // IFFT 8
+            if constexpr (!IFO) tab2<L, true, 9, S9>(wa, t, smem);
+            swap2<5>(XL, XH);
+            bfly2<false>(XL, XH, wb);  // IFFT 9
+            if constexpr (IFO) {
+                store_mid();
+                return;
+            }
+            if constexpr (GEN) col2_fd<S9, L, 9>(XL, XH, t, img);
+        } else {
+            tab2<L, true, 9, S9>(wa, t, smem);
+        }
         tab2<L, true, 8, S8>(wb, t, smem);
         bfly2<true>(XL, XH, wa);   // FFT 9
         tab2<L, true, 7, MM>(wa, t, smem);
@@ -989,13 +1057,21 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         if constexpr (GEN) __syncthreads();
     } else if constexpr (L == 9) {
         using S8 = typename SMap<L, 8>::M;
-        tab2<L, false, 8, S8>(wa, t, smem);
-        exchange2<S6, MM>(XL, XH, t, img);
-        bfly2<false>(XL, XH, wb);  // IFFT 7
-        tab2<L, true, 8, S8>(wb, t, smem);
-        swap2<4>(XL, XH);
-        bfly2<false>(XL, XH, wa);  // IFFT 8
-        if constexpr (GEN) col2_fd<S8, L, 8>(XL, XH, t, img);
+        if constexpr (!FFX) {
+            tab2<L, false, 8, S8>(wa, t, smem);
+            exchange2<S6, MM>(XL, XH, t, img);
+            bfly2<false>(XL, XH, wb);  // IFFT 7
+            if constexpr (!IFO) tab2<L, true, 8, S8>(wb, t, smem);
+            swap2<4>(XL, XH);
+            bfly2<false>(XL, XH, wa);  // IFFT 8
+            if constexpr (IFO) {
+                store_mid();
+                return;
+            }
+            if constexpr (GEN) col2_fd<S8, L, 8>(XL, XH, t, img);
+        } else {
+            tab2<L, true, 8, S8>(wb, t, smem);
+        }
         tab2<L, true, 7, MM>(wa, t, smem);
         bfly2<true>(XL, XH, wb);   // FFT 8
         tab2<L, true, 6, S6>(wb, t, smem);
@@ -1003,10 +1079,18 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         bfly2<true>(XL, XH, wa);   // FFT 7
         if constexpr (GEN) __syncthreads();
     } else {
-        tab2<L, true, 7, MM>(wa, t, smem);
-        exchange2<S6, MM>(XL, XH, t, img);
-        bfly2<false>(XL, XH, wb);  // IFFT 7
-        if constexpr (GEN) col2_fd<MM, L, 7>(XL, XH, t, img);
+        if constexpr (!FFX) {
+            if constexpr (!IFO) tab2<L, true, 7, MM>(wa, t, smem);
+            exchange2<S6, MM>(XL, XH, t, img);
+            bfly2<false>(XL, XH, wb);  // IFFT 7
+            if constexpr (IFO) {
+                store_mid();
+                return;
+            }
+            if constexpr (GEN) col2_fd<MM, L, 7>(XL, XH, t, img);
+        } else {
+            tab2<L, true, 7, MM>(wa, t, smem);
+        }
         tab2<L, true, 6, S6>(wb, t, smem);
         bfly2<true>(XL, XH, wa);   // FFT 7
         if constexpr (GEN) __syncthreads();
@@ -1050,7 +1134,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
             vl = zl;
             vh = zh;
         }
-        const bool st_ok = GEN ? lost[m] : r < a.out_rows;
+        const bool st_ok = GEN ? lost[m] : r < out_rows;
         if (st_ok) {
             uint32_t* p = (uint32_t*)(out + (size_t)(GEN && !a.rev_a ? r - a.chunk : r) * a.S_out);
             __builtin_nontemporal_store(vl, p);
@@ -1239,8 +1323,13 @@ hipError_t launch_col_multi(const ColArgs& a, bool high, hipStream_t s) {
 }
 
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
-    if (L < COL_LMIN || L > COL_LGEN || mode < COL_ENC || mode > COL_DEC_GEN) return hipErrorInvalidValue;
+    if (L < COL_LMIN || L > COL_LGEN || mode < COL_ENC || mode > COL_ENC_FFTX) return hipErrorInvalidValue;
     if (L == COL_LGEN && mode != COL_DEC_GEN) return hipErrorInvalidValue;
+    // multi-chunk encodes: radix-2 form, one stripe, nch <= COL_MAX_CHUNKS
+    const bool chunks = mode >= COL_ENC_IFFT || a.nch > 1;
+    if (chunks && (L < COL_LCHUNK || L > COL_LMAX || a.nstripes != 1 || a.nch == 0 || a.nch > COL_MAX_CHUNKS ||
+                   (mode != COL_ENC && mode < COL_ENC_IFFT)))
+        return hipErrorInvalidValue;
     if (a.qrow == 0 || a.nstripes == 0 || a.out_rows == 0) return hipSuccess;
     typedef void (*ColFn)(ColArgs);
 #define RS16_COL_ROW(L)                                                                                   \
@@ -1251,12 +1340,19 @@ hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
 #undef RS16_COL_ROW
     static const int lds[6] = {ColSmem<6>::BYTES, ColSmem<7>::BYTES,  ColSmem<8>::BYTES,
                                ColSmem<9>::BYTES, ColSmem<10>::BYTES, ColSmem<11>::BYTES};
-    ColFn fn = fns[L - COL_LMIN][mode];
-    if (!fn) return hipErrorInvalidValue;  // (the ework decoder needs 4 waves: L >= 9)
-    uint32_t threads = (1u << L) / 4;
-    // the encode and the half decode of 2^8 .. 2^10 rows: the radix-2 form
-    // (2 rows per thread), unless RS16_DIAG_COL_RADIX4
-    if (mode != COL_DEC_EWORK && L >= 8 && !(g_diag & DIAG_COL_RADIX4)) {
+    ColFn fn = mode <= COL_DEC_GEN ? fns[L - COL_LMIN][mode] : nullptr;
+    if (!fn && !chunks) return hipErrorInvalidValue;  // (the ework decoder needs 4 waves: L >= 9)
+    uint32_t threads = (1u << L) / 4, rows = 1;
+    if (chunks) {
+        static const ColFn fnc[3][3] = {{col2_kernel<8, COL_ENC>, col2_kernel<8, COL_ENC_IFFT>, col2_kernel<8, COL_ENC_FFTX>},
+                                        {col2_kernel<9, COL_ENC>, col2_kernel<9, COL_ENC_IFFT>, col2_kernel<9, COL_ENC_FFTX>},
+                                        {col2_kernel<10, COL_ENC>, col2_kernel<10, COL_ENC_IFFT>, col2_kernel<10, COL_ENC_FFTX>}};
+        fn = fnc[L - COL_LCHUNK][mode == COL_ENC ? 0 : mode - COL_ENC_IFFT + 1];
+        threads = (1u << L) / 2;
+        rows = mode == COL_ENC_FFTX ? 1 : a.nch;  // (one grid row per chunk)
+    } else if (mode != COL_DEC_EWORK && L >= 8 && !(g_diag & DIAG_COL_RADIX4)) {
+        // the encode and the half decode of 2^8 .. 2^10 rows: the radix-2
+        // form (2 rows per thread), unless RS16_DIAG_COL_RADIX4
         static const ColFn fns2[4][3] = {
             {col2_kernel<8, COL_ENC>, col2_kernel<8, COL_DEC_EVAL>, col2_kernel<8, COL_DEC_GEN>},
             {col2_kernel<9, COL_ENC>, col2_kernel<9, COL_DEC_EVAL>, col2_kernel<9, COL_DEC_GEN>},
@@ -1265,12 +1361,17 @@ hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
         fn = fns2[L - 8][mode == COL_ENC ? 0 : (mode == COL_DEC_EVAL ? 1 : 2)];
         threads = (1u << L) / 2;
     }
-    const int bytes = lds[L - COL_LMIN];
+    int bytes = lds[L - COL_LMIN];
+    if (chunks) {
+        static const int enc[3] = {ColSmem<8>::ELOG, ColSmem<9>::ELOG, ColSmem<10>::ELOG};
+        static const int ifo[3] = {ColSmem<8>::B, ColSmem<9>::B, ColSmem<10>::B};
+        bytes = (mode == COL_ENC_IFFT ? ifo : enc)[L - COL_LCHUNK];
+    }
     if (bytes > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3(threads), bytes, s, a);
+    hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes, rows), dim3(threads), bytes, s, a);
     return hipGetLastError();
 }
 

@@ -220,6 +220,15 @@ bool rs16_engine::col_ok(int L, size_t S, size_t nstripes, bool gen) const {
     return (S / 8) * nstripes <= col_max_quads || (g_diag & DIAG_FORCE_COLUMN);
 }
 
+// the radix-2 multi-chunk encodes (launch_col, COL_ENC_IFFT / COL_ENC_FFTX /
+// COL_ENC with nch > 1): 2^8 .. 2^10-row chunks, 2 or more of them and at
+// most col_max_chunk_rows rows
+bool rs16_engine::col_chunks_ok(int L, uint32_t nch, size_t S) const {
+    return L >= (int)COL_LCHUNK && L <= (int)COL_LMAX && nch > 1 && nch <= COL_MAX_CHUNKS &&
+           (((size_t)nch << L) <= col_max_chunk_rows || (g_diag & DIAG_FORCE_COLUMN)) &&
+           nch < col_img_count((uint32_t)L) && col_ok(L, S, 1);
+}
+
 ColArgs rs16_engine::col_args() const {
     ColArgs a;
     std::memset(&a, 0, sizeof a);
@@ -256,12 +265,14 @@ int rs16_engine::col_tables(hipStream_t s, rs16_error* err) {
 }
 
 int rs16_engine::col(const ColArgs& args, int L, int mode, hipStream_t s, rs16_error* err) {
-    const bool dec = mode != COL_ENC;
+    const bool dec = mode == COL_DEC_EWORK || mode == COL_DEC_EVAL || mode == COL_DEC_GEN;
     if (int rc = col_tables(s, err)) return rc;
-    // the table images of the two transforms (skew deltas 0 / 2^L only)
+    // the table images of the two transforms (skew deltas 0 / 2^L; the
+    // kernel adds the chunk index of a multi-chunk encode to the delta)
     ColArgs a = args;
     const uint32_t N = 1u << L;
-    if ((a.skew_ifft != 0 && a.skew_ifft != N) || (a.skew_fft != 0 && a.skew_fft != N))
+    if ((a.skew_ifft != 0 && a.skew_ifft != N) || (a.skew_fft != 0 && a.skew_fft != N) ||
+        (a.nch > 1 && a.nch >= col_img_count((uint32_t)L)))
         return hip_fail(err, hipErrorInvalidValue);  // (unreachable: every caller passes 0 or 2^L)
     a.img_ifft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_ifft ? 1 : 0));
     a.img_fft = (const uint8_t*)(d_col_img + col_img_offset((uint32_t)L, a.skew_fft ? 1 : 0));
@@ -757,6 +768,30 @@ int rs16_engine::encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, 
     }
     if (L == (int)COLM_L && nch <= COLM_MAX_CHUNKS && col_ok(L, S, 1))
         return col_multi(k, m, S, S_user, d_orig, d_rec, nch, true, s, err);
+    if (col_chunks_ok(L, nch, S)) {
+        // 256 / 512 / 1024-row chunks: every chunk's IFFT into Z (one
+        // workgroup per quad column and chunk), then the FFT of their XOR
+        ColArgs c = col_args();
+        c.in = d_orig;
+        c.S_in = S_user;
+        c.out = Z;
+        c.S_out = S;
+        c.qrow = (uint32_t)(S / 8);
+        c.in_rows = (uint32_t)k;
+        c.out_rows = (uint32_t)(nch * chunk);
+        c.skew_ifft = (uint32_t)chunk;
+        c.nch = nch;
+        if (int rc = col(c, L, COL_ENC_IFFT, s, err)) return rc;
+        c.in = Z;
+        c.S_in = S;
+        c.out = d_rec;
+        c.S_out = S_user;
+        c.in_rows = (uint32_t)(nch * chunk);
+        c.out_rows = (uint32_t)m;
+        c.skew_ifft = 0;
+        c.skew_fft = 0;
+        return col(c, L, COL_ENC_FFTX, s, err);
+    }
     PassArgs a = base_args(this, S);
     a.seg_a = d_orig;
     a.S_seg = S_user;
@@ -806,6 +841,21 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
     }
     if (nch > 1 && L == (int)COLM_L && nch <= COLM_MAX_CHUNKS && col_ok(L, S, 1))
         return col_multi(k, m, S, S_user, d_orig, d_rec, nch, false, s, err);
+    if (nch > 1 && col_chunks_ok(L, nch, S)) {
+        // 256 / 512 / 1024-row chunks: one launch, one workgroup per (quad
+        // column, recovery chunk), each running the originals' IFFT itself
+        ColArgs c = col_args();
+        c.in = d_orig;
+        c.out = d_rec;
+        c.S_in = c.S_out = S_user;
+        c.qrow = (uint32_t)(S / 8);
+        c.in_rows = (uint32_t)k;
+        c.out_rows = (uint32_t)m;
+        c.skew_ifft = 0;
+        c.skew_fft = (uint32_t)chunk;
+        c.nch = nch;
+        return col(c, L, COL_ENC, s, err);
+    }
     // U belongs to the caller's stream (no engine-wide fallback: two calls
     // on concurrent streams sharing one buffer restored wrong data, round 3)
     if (!U) return set_error(err, RS16_INVALID_ARGUMENT);

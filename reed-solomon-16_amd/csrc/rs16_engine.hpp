@@ -222,6 +222,13 @@ struct rs16_engine {
     // twiddle table over 32 quad columns.
     uint32_t col_max_quads = 256;  // (measured: scripts/probe_col.py)
     bool col_ok(int L, size_t S, size_t nstripes, bool gen = false) const;  // gen: the general decode (up to 2^11 rows)
+    // Multi-chunk encodes of 2^8 .. 2^10-row chunks in the column codec: at
+    // most col_max_chunk_rows rows in all (more take the passes: every
+    // workgroup stages its own twiddle tables, and the low rate's repeats the
+    // IFFT, so the column form's cost grows faster with the chunk count;
+    // break-even 6-8 chunks of 1024 rows, scripts/probe_chunks.py)
+    uint32_t col_max_chunk_rows = 6144;
+    bool col_chunks_ok(int L, uint32_t nch, size_t S) const;
     int col(const rs16::ColArgs& a, int L, int mode, hipStream_t s, rs16_error* err);
     int col_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec, uint32_t nch,
                   bool high, hipStream_t s, rs16_error* err);

@@ -17,9 +17,11 @@ struct HostTables {
     std::vector<uint32_t> mul_tab;     // TAB_ENTRIES * TAB_DWORDS
     std::vector<uint32_t> skew_tab;    // GF_ORDER * TAB_DWORDS: mul_tab row of skew_entry[i]
     // Column codec (rs16_col.hip): the 2^L - 1 twiddle tables (20 dwords
-    // each, tile-group order) of a 2^L-row transform at skew delta 0 or 2^L,
-    // contiguous, for L = COL_LMIN .. COL_LMAX; image (L, d) at
-    // col_img_offset(L, d) dwords.
+    // each, tile-group order) of a 2^L-row transform at skew delta d 2^L,
+    // contiguous, for L = COL_LMIN .. COL_LGEN and d < col_img_count(L);
+    // image (L, d) at col_img_offset(L, d) dwords.  (The images of one L
+    // together are a permutation of the twiddle indices [0, 65535) when d
+    // covers every chunk: the multi-chunk codecs of 2^8 .. 2^10 rows.)
     std::vector<uint32_t> col_img;
     // eval_poly of a high-rate decode with n = 2^(L+1) <= 2048 work rows as
     // an n-point XOR convolution (rs16_col.hip): col_v[col_v_offset(n) + k] =
@@ -31,14 +33,20 @@ struct HostTables {
     std::vector<uint32_t> col_k;
 };
 constexpr uint32_t COL_LMIN = 6, COL_LMAX = 10;
+// (and the general decoder's 2^11-row transform, skew delta 0 only)
+constexpr uint32_t COL_LGEN = 11;
+// L = 8 .. 10 (the radix-2 codec's multi-chunk encodes): every delta d 2^L
+// (d < 2^(16 - L)); 6, 7: d = 0, 1; 11: d = 0
+constexpr uint32_t COL_LCHUNK = 8;
+constexpr uint32_t col_img_count(uint32_t L) {
+    return L == COL_LGEN ? 1u : (L >= COL_LCHUNK ? (1u << (16 - L)) : 2u);
+}
 constexpr size_t col_img_offset(uint32_t L, uint32_t d) {
     size_t off = 0;
-    for (uint32_t l = COL_LMIN; l < L; l++) off += 2 * ((1u << l) - 1) * 20;
+    for (uint32_t l = COL_LMIN; l < L; l++) off += (size_t)col_img_count(l) * ((1u << l) - 1) * 20;
     return off + (size_t)d * ((1u << L) - 1) * 20;
 }
-// (and the general decoder's 2^11-row transform, skew delta 0 only, after them)
-constexpr uint32_t COL_LGEN = 11;
-constexpr size_t COL_IMG_DWORDS = col_img_offset(COL_LGEN, 0) + ((1u << COL_LGEN) - 1) * 20;
+constexpr size_t COL_IMG_DWORDS = col_img_offset(COL_LGEN + 1, 0);
 // n = 2^COL_LMIN .. 2^(COL_LMAX+1): tables of n entries at n - 2^COL_LMIN
 constexpr size_t col_v_offset(uint32_t n) { return n - (1u << COL_LMIN); }
 constexpr size_t COL_V_DWORDS = col_v_offset(4u << COL_LMAX);
@@ -216,13 +224,21 @@ struct ColArgs {
     // bs_flags_o bytes, elog + st bs_elog words (0: shared by all stripes)
     uint64_t bs_flags, bs_flags_o;
     uint32_t bs_elog;
-    uint32_t nch;               // launch_col_multi: chunks of 128 rows (one wave each)
+    uint32_t nch;               // launch_col_multi: chunks of 128 rows (one wave each); launch_col: chunks (ColMode)
     uint64_t* stamps;           // RS16_STAMPS builds: phase timeline (rs16_engine_set_stamps)
 };
 int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec covers
 // COL_DEC_GEN: the general high-rate decode of a 2^L-row work buffer (any
 // loss pattern; formal derivative in the kernel), polynomial in the kernel
-enum ColMode : int { COL_ENC = 0, COL_DEC_EWORK, COL_DEC_EVAL, COL_DEC_GEN };
+//   COL_ENC_IFFT / COL_ENC_FFTX (2^8 .. 2^10 rows): the high rate's
+//   multi-chunk encode in two launches -- the IFFT of every chunk of
+//   originals (grid row = chunk, skew_ifft = 2^L: chunk c at delta (c + 1)
+//   2^L) stored whole, then the FFT (skew 0) of the XOR of nch chunks
+// ColArgs::nch > 1 with COL_ENC / COL_ENC_IFFT: one grid row per chunk (COL_ENC:
+// the low rate's recovery chunks, FFT of chunk c at delta (c + 1) 2^L)
+enum ColMode : int { COL_ENC = 0, COL_DEC_EWORK, COL_DEC_EVAL, COL_DEC_GEN, COL_ENC_IFFT, COL_ENC_FFTX };
+// the radix-2 multi-chunk encodes take at most this many chunks (more: passes)
+constexpr uint32_t COL_MAX_CHUNKS = 64;
 hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s);
 // Multi-chunk encodes of 128-row chunks in one launch (colm_kernel): high
 // rate (high = 1: nch chunks of originals, one recovery chunk) or low rate
@@ -238,7 +254,7 @@ enum DiagFlags : int {
     DIAG_EVAL_TWO_KERNEL = 2, // eval_poly: two-kernel form even when the one-kernel form applies
     DIAG_EVAL_FULL = 4,       // eval_poly: the full 65536-point form even for n <= 2048
     DIAG_NO_COLUMN = 8,       // 2^9 / 2^10-row transforms through the pass codec (rs16_col.hip off)
-    DIAG_FORCE_COLUMN = 16,   // ... through the column codec at any width (rs16_engine::col_max_quads ignored)
+    DIAG_FORCE_COLUMN = 16,   // ... through the column codec at any width (rs16_engine::col_max_quads, col_max_chunk_rows ignored)
     DIAG_TILE_LAST = 32,      // the general decode's T = 8 last pass as tile_last_kernel at any loss count
     DIAG_NO_TILE_LAST = 64,   // ... always as the 8-wave pass (DEC_LAST items)
     DIAG_FD_LDS = 128,        // DEC_MID's in-tile formal derivative always through the LDS image (tile_fd)

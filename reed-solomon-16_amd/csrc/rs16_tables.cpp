@@ -133,8 +133,8 @@ void build(HostTables& t) {
     // index j 2^(kb+1) + 2^kb + delta - 1 (engine_naive.rs:43-124).
     t.col_img.assign(COL_IMG_DWORDS, 0);
     for (uint32_t L = COL_LMIN; L <= COL_LGEN; L++)
-        for (uint32_t d = 0; d < (L == COL_LGEN ? 1u : 2u); d++) {
-            const uint32_t N = 1u << L, delta = d ? N : 0;
+        for (uint32_t d = 0; d < col_img_count(L); d++) {
+            const uint32_t N = 1u << L, delta = d * N;
             uint32_t* img = &t.col_img[col_img_offset(L, d)];
             for (uint32_t g = 0; g + 1 < N; g++) {
                 uint32_t kb = 0;

@@ -313,3 +313,28 @@ def test_col_multi_chunk_encode(eng, k, m, sb):
         assert np.array_equal(dev_encode(eng, original, m), got)
     finally:
         rs16.set_diagnostics(old)
+
+
+@pytest.mark.parametrize("k,m", [(3000, 1000), (1025, 1000), (2000, 300), (1500, 200), (10000, 1000), (40000, 1000),
+                                 (1000, 3000), (1000, 1025), (300, 2000), (200, 1500), (1000, 10000), (1000, 40000)])
+@pytest.mark.parametrize("sb", [64, 1024])
+def test_col_chunks_encode(eng, k, m, sb):
+    # multi-chunk encodes of 256 / 512 / 1024-row chunks in the radix-2
+    # column codec (rate_high.rs:44-83: every chunk's IFFT, then the FFT of
+    # their XOR -- two launches; rate_low.rs:44-83: one launch, a workgroup
+    # per quad column and recovery chunk); partial last chunks, and up to 40
+    # chunks (beyond the codec's default chunk-row limit: forced,
+    # RS16_DIAG_FORCE_COLUMN).  Equal to the oracle and to the pass codec
+    # (RS16_DIAG_NO_COLUMN).
+    original = generate_original(k, sb, 7 * k + m + sb)
+    old = rs16.set_diagnostics(rs16.DIAG_FORCE_COLUMN)
+    try:
+        got = dev_encode(eng, original, m)
+    finally:
+        rs16.set_diagnostics(old)
+    assert np.array_equal(got, O.encode(k, m, original))
+    old = rs16.set_diagnostics(rs16.DIAG_NO_COLUMN)
+    try:
+        assert np.array_equal(dev_encode(eng, original, m), got)
+    finally:
+        rs16.set_diagnostics(old)
