@@ -1136,9 +1136,11 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         }
         const bool st_ok = GEN ? lost[m] : r < out_rows;
         if (st_ok) {
+            // (plain stores: same-box A/B against non-temporal ones, 3 pairs:
+            // 1000:1000 decode 11.38 -> 11.18 us, 512:512 7.55 -> 7.40)
             uint32_t* p = (uint32_t*)(out + (size_t)(GEN && !a.rev_a ? r - a.chunk : r) * a.S_out);
-            __builtin_nontemporal_store(vl, p);
-            __builtin_nontemporal_store(vh, p + 8);
+            p[0] = vl;
+            p[8] = vh;
         }
     }
     cstamp(a, 10);
