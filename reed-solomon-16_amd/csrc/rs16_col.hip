@@ -910,8 +910,8 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             uint32_t* p = (uint32_t*)(out + (size_t)FM::row(t, m) * a.S_out);
-            __builtin_nontemporal_store(XL[m], p);
-            __builtin_nontemporal_store(XH[m], p + 8);
+            p[0] = XL[m];
+            p[8] = XH[m];
         }
     };
     if constexpr (!DEC) dma_tables();
@@ -1298,8 +1298,8 @@ __global__ __launch_bounds__(1024) void colm_kernel(ColArgs a) {
         const uint32_t r = (HI ? 0u : c * CM_N) + S0::row(lane, m);
         if (r < a.out_rows) {
             uint32_t* p = (uint32_t*)(out + (size_t)r * a.S_out);
-            __builtin_nontemporal_store(XL[m], p);
-            __builtin_nontemporal_store(XH[m], p + 8);
+            p[0] = XL[m];
+            p[8] = XH[m];
         }
     }
 }

@@ -1642,8 +1642,10 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
         mul_xor(ol, oh, YL[m], YH[m], rt[m]);
         const int64_t rr = (int64_t)(tile << T) + 4 * lane + m + shift;
         uint32_t* p = (uint32_t*)(a.rest + rr * (int64_t)a.S_rest + offL);
-        __builtin_nontemporal_store(ol, p);
-        __builtin_nontemporal_store(oh, p + 8);
+        // (plain stores: 32768:32768 1 %-loss decode 103.1 -> 101.5 us against
+        // non-temporal ones, same-box A/B x 3)
+        p[0] = ol;
+        p[8] = oh;
     }
 }
 

@@ -24,6 +24,13 @@ def arm():
                            "enc_k": r["encode"]["kernel_us"], "dec_k": r["decode"]["kernel_us"]}
     for k, m in ((1000, 1000), (100, 1000)):
         out[f"{k}:{m} 1%"] = pc.run_1pct(eng, k, m, 1024, 0)
+    if os.environ.get("AB_WIDE"):
+        # multi-chunk encodes (colm_kernel / chunked col2_kernel) and the
+        # 1 %-loss decode at 32768:32768 (tile_last_kernel)
+        for k, m in ((100, 1000), (1000, 100), (3000, 1000)):
+            r = pc.run(eng, k, m, 1024, 0)
+            out[f"{k}:{m}"] = {"exact": r["exact"], "enc": r["encode"]["host_us"]}
+        out["32768:32768 1%"] = pc.run_1pct(eng, 32768, 32768, 1024, 0)
     print(json.dumps(out), flush=True)
 
 
