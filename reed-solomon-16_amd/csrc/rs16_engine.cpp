@@ -222,10 +222,13 @@ bool rs16_engine::col_ok(int L, size_t S, size_t nstripes, bool gen) const {
 
 // the radix-2 multi-chunk encodes (launch_col, COL_ENC_IFFT / COL_ENC_FFTX /
 // COL_ENC with nch > 1): 2^8 .. 2^10-row chunks, 2 or more of them and at
-// most col_max_chunk_rows rows
-bool rs16_engine::col_chunks_ok(int L, uint32_t nch, size_t S) const {
+// most col_max_chunk_rows rows (the high rate's 256 / 512-row chunks: up to
+// 8192 rows, which still beat the passes there: 8000:300 30.1 against 33.7
+// us, 8000:200 34.0 against 40.9, profiles/r04_probe_chunks.txt)
+bool rs16_engine::col_chunks_ok(int L, uint32_t nch, size_t S, bool high) const {
+    const size_t rows_max = high && L <= 9 ? std::max<size_t>(col_max_chunk_rows, 8192) : col_max_chunk_rows;
     return L >= (int)COL_LCHUNK && L <= (int)COL_LMAX && nch > 1 && nch <= COL_MAX_CHUNKS &&
-           (((size_t)nch << L) <= col_max_chunk_rows || (g_diag & DIAG_FORCE_COLUMN)) &&
+           (((size_t)nch << L) <= rows_max || (g_diag & DIAG_FORCE_COLUMN)) &&
            nch < col_img_count((uint32_t)L) && col_ok(L, S, 1);
 }
 
@@ -768,7 +771,7 @@ int rs16_engine::encode_high_multi(size_t k, size_t m, size_t S, size_t S_user, 
     }
     if (L == (int)COLM_L && nch <= COLM_MAX_CHUNKS && col_ok(L, S, 1))
         return col_multi(k, m, S, S_user, d_orig, d_rec, nch, true, s, err);
-    if (col_chunks_ok(L, nch, S)) {
+    if (col_chunks_ok(L, nch, S, true)) {
         // 256 / 512 / 1024-row chunks: every chunk's IFFT into Z (one
         // workgroup per quad column and chunk), then the FFT of their XOR
         ColArgs c = col_args();
@@ -841,7 +844,7 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
     }
     if (nch > 1 && L == (int)COLM_L && nch <= COLM_MAX_CHUNKS && col_ok(L, S, 1))
         return col_multi(k, m, S, S_user, d_orig, d_rec, nch, false, s, err);
-    if (nch > 1 && col_chunks_ok(L, nch, S)) {
+    if (nch > 1 && col_chunks_ok(L, nch, S, false)) {
         // 256 / 512 / 1024-row chunks: one launch, one workgroup per (quad
         // column, recovery chunk), each running the originals' IFFT itself
         ColArgs c = col_args();

@@ -228,7 +228,7 @@ struct rs16_engine {
     // IFFT, so the column form's cost grows faster with the chunk count;
     // break-even 6-8 chunks of 1024 rows, scripts/probe_chunks.py)
     uint32_t col_max_chunk_rows = 6144;
-    bool col_chunks_ok(int L, uint32_t nch, size_t S) const;
+    bool col_chunks_ok(int L, uint32_t nch, size_t S, bool high) const;
     int col(const rs16::ColArgs& a, int L, int mode, hipStream_t s, rs16_error* err);
     int col_multi(size_t k, size_t m, size_t S, size_t S_user, const uint8_t* d_orig, uint8_t* d_rec, uint32_t nch,
                   bool high, hipStream_t s, rs16_error* err);
