@@ -353,8 +353,30 @@ def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
     t_all = timed(step, n4)
     t_codec = timed(codec, n4)
     t_coll = timed(lambda: (scatter_orig(), gather_rec(), scatter_rec(), gather_out()), n4)
+    # Each collective on its own: the bytes that cross
+    # the links (every column but the root's own slice: rows x (S - w_root)),
+    # the achieved rate over the root's links and per peer link, and the
+    # root's own pitched slice copy (rows x w_root, the only data movement at
+    # one rank).
+    w0 = rs16.column_slice(S4, world, 0)[1]
+    peers = world - 1
+    coll = {}
+    for name, fn, rows in (("scatter_originals", scatter_orig, k), ("gather_recovery", gather_rec, m),
+                           ("scatter_recovery", scatter_rec, m), ("gather_originals", gather_out, k)):
+        t = timed(fn, n4) / n4
+        link_bytes = rows * (S4 - w0) if peers else 0
+        coll[name] = {"ms": t * 1e3, "link_bytes": link_bytes,
+                      "root_links_gb_s": link_bytes / t / 1e9 if peers else None,
+                      "per_peer_gb_s": link_bytes / peers / t / 1e9 if peers else None,
+                      "root_own_slice_bytes": rows * w0, "root_own_slice_gb_s": rows * w0 / t / 1e9}
     comm.close()
     step_bytes = 2 * (k + m) * S4
+    # The root sends (scatters) and receives (gathers) every column but its
+    # own: 2 (k + m) (S - w_root) bytes a step, over min(N - 1, 7) xGMI links
+    # of ~153 GB/s each (point to point; one direction per phase, the phases
+    # in sequence), plus the codec on 1 / N of the columns per rank.
+    link_gbs = 153.0
+    bound_ms = (2 * (k + m) * (S4 - w0) / (min(peers, 7) * link_gbs * 1e9) * 1e3) if peers else 0.0
     return {
         "workload": f"{k}:{m} x {S4} B stripe in rank 0's HBM, byte columns split over {world} rank(s) "
                     f"({w} B each) with RCCL scatter/gather; encode + 100%-loss decode (BASELINE configs[4])",
@@ -363,8 +385,76 @@ def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
         "collectives_ms": t_coll / n4 * 1e3,
         # scatter originals (k rows) + gather recovery (m) + scatter recovery (m)
         # + gather originals (k), each moving every column but the root's own slice
-        "collective_bytes_per_step": 2 * (k + m) * (S4 - rs16.column_slice(S4, world, 0)[1]) if world > 1 else 0,
+        "collective_bytes_per_step": 2 * (k + m) * (S4 - w0) if peers else 0,
+        "collectives": coll,
+        "root_link_bound_ms": bound_ms,
+        "root_link_bound_note": f"2 (k + m) (S - w_root) bytes through rank 0 over min(N-1, 7) links x {link_gbs} GB/s",
+        "expected_step_ms_at_link_bound": bound_ms + t_codec / n4 * 1e3,
         "restored_stripe_verified": ok, "whole_configs4": world == 8}
+
+
+def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
+    """Serving mode (not the metric): two independent stripes per step, one
+    per engine / stream, so that one stripe's load and store phases overlap
+    the other's butterflies; and the producer / consumer form, engine A
+    encoding a stripe while engine B decodes another one's (already encoded)
+    recovery.  Both restorations are checked."""
+    import numpy as np
+
+    import rs16
+    from rs16.device import DeviceArray
+    from rs16.util import generate_original
+
+    eng2 = rs16.Engine(local)
+    o2 = generate_original(k, S, 1)
+    a2, r2, x2 = DeviceArray.from_numpy(eng2, o2), DeviceArray(eng2, m * S), DeviceArray(eng2, k * S)
+    f2o, f2r = DeviceArray.from_numpy(eng2, of), DeviceArray.from_numpy(eng2, rf)
+    if loss < k:
+        x2.upload(o2)
+
+    def enc2():
+        rs16.encode_device(k, m, S, a2.ptr, r2.ptr, engine=eng2)
+
+    def dec2():
+        rs16.decode_device(k, m, S, x2.ptr, f2o.ptr, r2.ptr, f2r.ptr, k - loss, loss, engine=eng2)
+
+    def two():
+        encode()
+        enc2()
+        decode()
+        dec2()
+
+    def enc_dec():
+        encode()
+        dec2()
+
+    def run(body, steps):
+        for _ in range(args.warmup):
+            body()
+        eng.synchronize()
+        eng2.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            body()
+        eng.synchronize()
+        eng2.synchronize()
+        return time.perf_counter() - t0
+
+    two()
+    eng2.synchronize()
+    assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
+    step_bytes = 2 * (k + m) * S
+    t2 = run(two, args.steps)
+    t3 = run(enc_dec, args.steps)
+    assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
+    del a2, r2, x2, f2o, f2r
+    eng2.close()
+    return {"gib_s": 2 * step_bytes * args.steps / t2 / GIB, "ms_per_two_stripes": t2 / args.steps * 1e3,
+            "encode_while_decode_gib_s": step_bytes * args.steps / t3 / GIB,
+            "encode_while_decode_us": t3 / args.steps * 1e6, "where": where,
+            "note": "serving-mode throughput: two independent 32768:32768 x 1 KiB stripes in flight "
+                    "(gib_s), or one stripe encoding on engine A while another's recovery decodes on "
+                    "engine B (encode_while_decode); not the metric"}
 
 
 def main():
@@ -496,6 +586,11 @@ def main():
     # Separate encode-only / decode-only rates (same data, same engine).
     dt_e = timed(encode, args.steps)
     dt_d = timed(decode, args.steps)
+    two_early = None
+    if not args.no_extra and world == 1:
+        # the serving-mode rate measured right here as well as after the
+        # other extras: VERDICT r4 item 1 (probe 900 vs bench 756 GiB/s)
+        two_early = two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, "right after the timed loop")
     kernels = {name: {"avg_us": ms / n * 1e3, "launches": n} for name, (ms, n) in prof.items()}
     dom = max(prof, key=lambda p: prof[p][0])
     dom_avg_s = prof[dom][0] / prof[dom][1] / 1e3
@@ -722,40 +817,9 @@ def main():
         extra["configs4_rccl"] = configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, args.steps)
 
     if not args.no_extra and world == 1:
-        # Serving mode (not the metric): two independent stripes per step, one
-        # per engine / stream, so that one stripe's load and store phases
-        # overlap the other's butterflies.  Both restorations are checked.
-        eng2 = rs16.Engine(local)
-        o2 = generate_original(k, S, 1)
-        a2, r2, x2 = DeviceArray.from_numpy(eng2, o2), DeviceArray(eng2, m * S), DeviceArray(eng2, k * S)
-        f2o, f2r = DeviceArray.from_numpy(eng2, of), DeviceArray.from_numpy(eng2, rf)
-        if loss < k:
-            x2.upload(o2)
-
-        def two():
-            encode()
-            rs16.encode_device(k, m, S, a2.ptr, r2.ptr, engine=eng2)
-            decode()
-            rs16.decode_device(k, m, S, x2.ptr, f2o.ptr, r2.ptr, f2r.ptr, k - loss, loss, engine=eng2)
-
-        two()
-        eng2.synchronize()
-        assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
-        for _ in range(args.warmup):
-            two()
-        eng.synchronize()
-        eng2.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            two()
-        eng.synchronize()
-        eng2.synchronize()
-        t2 = time.perf_counter() - t0
-        extra["two_stripes_two_streams"] = {
-            "gib_s": 2 * step_bytes * args.steps / t2 / GIB, "ms_per_two_stripes": t2 / args.steps * 1e3,
-            "note": "serving-mode throughput, two independent 32768:32768 x 1 KiB stripes in flight; not the metric"}
-        del a2, r2, x2, f2o, f2r
-        eng2.close()
+        extra["two_stripes_two_streams"] = two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args,
+                                                       "after the other extras (the r04 position)")
+        extra["two_stripes_two_streams"]["right_after_timed_loop"] = two_early
 
     if not args.no_extra:
         # Shards that start and end in host memory (north_star: recorded beside
@@ -786,6 +850,44 @@ def main():
             "encode_gib_s": world * (k + m) * S * n3 / te / GIB, "decode_gib_s": world * (k + m) * S * n3 / td / GIB,
             "encode_us": te / n3 * 1e6, "decode_us": td / n3 * 1e6,
             "path": "pinned host buffers -> H2D -> device codec -> D2H (rs16_encode_host / rs16_decode_host)"}
+        del h_orig, h_rec, h_rest
+        # Several stripes, two in flight (rs16_encode_host_batch /
+        # rs16_decode_host_batch): stripe i + 1's H2D and stripe i - 1's D2H
+        # overlap stripe i's codec, so both link directions carry data.  Every
+        # stripe holds this stripe's data: each recovery must equal the one
+        # checked against the oracle fixture above, each decode restore it.
+        nb = 8
+        hb_o, hb_r = PinnedArray(eng, nb * k * S), PinnedArray(eng, nb * m * S)
+        hb_o.array.reshape(nb, k * S)[:] = original.reshape(1, -1)
+        fob = np.tile(of, nb)
+        frb = np.tile(rf, nb)
+
+        def batch_encode():
+            rs16.encode_host_batch(k, m, S, nb, hb_o.ptr, k * S, hb_r.ptr, m * S, engine=eng)
+
+        def batch_decode():
+            rs16.decode_host_batch(k, m, S, nb, hb_o.ptr, k * S, fob, k, hb_r.ptr, m * S, frb, m, engine=eng)
+
+        batch_encode()
+        assert all(np.array_equal(hb_r.array.reshape(nb, m, S)[i], recovery) for i in range(nb)), \
+            "pipelined host encode differs"
+        hb_o.array.reshape(nb, k, S)[:, :loss] = 0
+        batch_decode()
+        assert all(np.array_equal(hb_o.array.reshape(nb, k, S)[i], original) for i in range(nb)), \
+            "pipelined host decode did not restore"
+        n5 = max(3, args.steps // 4)
+        tbe = timed(batch_encode, n5)
+        tbd = timed(batch_decode, n5)
+        extra["host_batch_pipelined"] = {
+            "stripes_per_call": nb,
+            "encode_gib_s": world * nb * (k + m) * S * n5 / tbe / GIB,
+            "decode_gib_s": world * nb * (k + m) * S * n5 / tbd / GIB,
+            "encode_ms_per_call": tbe / n5 * 1e3, "decode_ms_per_call": tbd / n5 * 1e3,
+            "link_bytes_per_call": {"encode": nb * (k + m) * S, "decode_100pct": nb * (k + loss) * S},
+            "path": "pinned host stripes, two in flight: H2D of stripe i+1 and D2H of stripe i-1 on two copy "
+                    "streams around stripe i's codec (rs16_encode_host_batch / rs16_decode_host_batch); "
+                    "every stripe's recovery == the fixture-checked one, every decode restored"}
+        del hb_o, hb_r
 
     if not args.no_extra and world == 1:
         # The reference's own API benchmark (ReedSolomonEncoder / Decoder with

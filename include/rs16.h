@@ -308,6 +308,32 @@ int rs16_decode_host(rs16_engine* eng, size_t original_count, size_t recovery_co
                      void* h_original, const uint8_t* original_received, const void* h_recovery,
                      const uint8_t* recovery_received, size_t slice_bytes, rs16_error* err);
 
+/* ---- Host-resident stripes, pipelined (full duplex) -----------------------
+ * nstripes independent stripes in host memory (stripe i's originals at
+ * h_original + i original_stride, its recovery at h_recovery + i
+ * recovery_stride; page-locked memory for DMA-rate copies), each encoded /
+ * decoded exactly as rs16_encode_host / rs16_decode_host would, with two
+ * stripes in flight: the host->device copy of stripe i + 1 and the
+ * device->host copy of stripe i - 1 run on two copy streams while stripe i
+ * is on the device, so both directions of the link carry data at once (one
+ * stripe alone cannot overlap: its outputs exist only after its inputs are
+ * all in).  Copies are contiguous row runs, no pitched copies.  The
+ * reference's EncoderWork / DecoderWork path (src/rate/encoder_work.rs:49-69,
+ * src/encoder_result.rs:31-95) once per stripe.  Synchronous.  Decode: stripe
+ * i's host flag bytes at original_received + i original_received_stride /
+ * recovery_received + i recovery_received_stride; only received rows travel
+ * to the device and only the lost originals come back (restored in place);
+ * a stripe with too few shards fails the whole call before any copy
+ * (NotEnoughShards, the first such stripe). */
+int rs16_encode_host_batch(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                           size_t nstripes, const void* h_original, size_t original_stride, void* h_recovery,
+                           size_t recovery_stride, rs16_error* err);
+int rs16_decode_host_batch(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                           size_t nstripes, void* h_original, size_t original_stride,
+                           const uint8_t* original_received, size_t original_received_stride,
+                           const void* h_recovery, size_t recovery_stride, const uint8_t* recovery_received,
+                           size_t recovery_received_stride, rs16_error* err);
+
 /* ---- Several GPUs in one process ------------------------
  * reed_solomon_16::encode / decode of ONE stripe with host-resident shards,
  * its byte columns split over the n engines (one per GPU): engine j takes its
@@ -403,9 +429,11 @@ int rs16_prog_count(void);
 int rs16_engine_set_stamps(rs16_engine* eng, void* d_buf, int prog, rs16_error* err);
 const char* rs16_prog_name(int prog);
 
-/* Diagnostics: process-wide switches to alternative code paths, for tests
- * and measurements only (results are identical; 0 = the shipped paths).
- * Returns the previous flags.  Not thread-safe against concurrent calls. */
+/* Diagnostics: switches of ONE engine to alternative code paths, for tests
+ * and measurements only (results are identical; 0 = the shipped paths, the
+ * state of every new engine).  Returns the engine's previous flags.  There is
+ * no process-wide state: other engines keep their own flags.  Like every call
+ * on an engine, not to be made while another thread issues work on it. */
 enum {
     RS16_DIAG_FORCE_VOFF64 = 1,    /* 64-bit per-lane HBM offsets in every pass */
     RS16_DIAG_EVAL_TWO_KERNEL = 2, /* eval_poly: the two-kernel form everywhere */
@@ -419,7 +447,7 @@ enum {
     RS16_DIAG_FD_LDS = 128,        /* the general decode's in-tile formal derivative always through LDS */
     RS16_DIAG_COL_RADIX4 = 256     /* column codec: 4 rows per thread everywhere (no radix-2 form) */
 };
-int rs16_set_diagnostics(int flags);
+int rs16_engine_set_diagnostics(rs16_engine* eng, int flags);
 
 /* Diagnostics: host-side evaluation of the device multiply (same v_perm
  * byte-table format and code path as the kernels, with v_perm emulated):

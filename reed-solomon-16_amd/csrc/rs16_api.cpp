@@ -123,13 +123,12 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
     const DecodeGeom& g = e->last_dec;
     uint64_t a = 0, b = 0;
     if (e->last_dec_flags_only) {
-        // nothing was restored and no kernel counted: count the flags here
-        // (the caller's arrays, as they are now; segment A / B sizes)
-        std::vector<uint8_t> f(std::max(g.a_count, g.b_count));
-        RS16_HIP(hipMemcpy(f.data(), e->last_flags_a, g.a_count, hipMemcpyDeviceToHost));
+        // nothing was restored and no kernel counted: count the copy of the
+        // flags the decode took (note_flags_only; segment A / B sizes)
+        std::vector<uint8_t> f(2 * (size_t)GF_ORDER);
+        RS16_HIP(hipMemcpy(f.data(), e->ws_flags.p, f.size(), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < g.a_count; i++) a += f[i] != 0;
-        RS16_HIP(hipMemcpy(f.data(), e->last_flags_b, g.b_count, hipMemcpyDeviceToHost));
-        for (uint32_t i = 0; i < g.b_count; i++) b += f[i] != 0;
+        for (uint32_t i = 0; i < g.b_count; i++) b += f[GF_ORDER + i] != 0;
     } else {
         const size_t chunks = ((size_t)g.n + 63) / 64;
         std::vector<uint32_t> c(2 * chunks);
@@ -142,9 +141,9 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
     if (got_o != want_o || got_r != want_r) return set_error(err, RS16_INVALID_ARGUMENT, got_o, got_r);
     return set_error(err, RS16_OK);
 }
-extern "C" int rs16_set_diagnostics(int flags) {
-    const int old = g_diag;
-    g_diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN |
+extern "C" int rs16_engine_set_diagnostics(rs16_engine* e, int flags) {
+    const int old = e->diag;
+    e->diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN |
                       DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4);
     return old;
 }
@@ -271,6 +270,7 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->ws_work32.release();
     e->ws_elog.release();
     e->ws_flags.release();
+    e->hp_flags.release();
     e->ws_zflag.release();
     e->ws_rbits.release();
     e->ws_lost.release();
@@ -281,6 +281,9 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     }
     e->hflags.release();
     if (e->hev) (void)hipEventDestroy(e->hev);
+    for (auto& row : e->hp_ev)
+        for (auto& ev : row)
+            if (ev) (void)hipEventDestroy(ev);
     if (e->order_ev) (void)hipEventDestroy(e->order_ev);
     for (int j = 0; j < rs16_engine::MAX_SLICES; j++) {
         if (e->sl_own[j]) (void)hipStreamDestroy(e->sl_own[j]);
@@ -1074,6 +1077,218 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
 }
 
 // ---------------------------------------------------------------------------
+// Host-resident stripes, pipelined.  Three streams: hslot[0].s copies inputs
+// in, the engine stream runs the codec, hslot[1].s copies outputs back.
+// Device buffers alternate by stripe parity b (hslot[b].orig / .rec; the
+// codec's scratch ws_z / ws_u is used only on the engine stream).  Stripe i:
+//   H2D  : [i >= 2: wait codec(i - 2) done with buffers b; decode: and its
+//          D2H, which reads the originals restored in place] copy in, record h2d[b]
+//   codec: wait h2d[b] [, i >= 2: wait d2h(i - 2) done reading buffers b]
+//          encode / decode, record codec[b]
+//   D2H  : wait codec[b], copy out, record d2h[b]
+// (a hipStreamWaitEvent waits for the event's latest record at the time of
+// the wait, which the enqueue order above makes the right stripe's).
+// ---------------------------------------------------------------------------
+int rs16_engine::host_pipe_events(rs16_error* err) {
+    for (auto& row : hp_ev)
+        for (auto& ev : row)
+            if (!ev) RS16_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    return RS16_OK;
+}
+
+namespace {
+enum { HP_H2D = 0, HP_CODEC = 1, HP_D2H = 2 };
+// Contiguous runs of rows whose flag equals `want` (rows [0, n)), each one
+// copy; more than max_runs of them: one copy of the span from the first to
+// the last such row.
+template <class F>
+int copy_runs(const uint8_t* flags, size_t n, bool want, size_t max_runs, F copy) {
+    size_t runs = 0, first = n, last = 0;
+    for (size_t i = 0; i < n;) {
+        if ((flags[i] != 0) != want) {
+            i++;
+            continue;
+        }
+        size_t j = i;
+        while (j < n && (flags[j] != 0) == want) j++;
+        runs++;
+        first = std::min(first, i);
+        last = j;
+        i = j;
+    }
+    if (runs == 0) return RS16_OK;
+    if (runs > max_runs) return copy(first, last - first);
+    for (size_t i = 0; i < n;) {
+        if ((flags[i] != 0) != want) {
+            i++;
+            continue;
+        }
+        size_t j = i;
+        while (j < n && (flags[j] != 0) == want) j++;
+        if (int rc = copy(i, j - i)) return rc;
+        i = j;
+    }
+    return RS16_OK;
+}
+constexpr size_t HP_MAX_RUNS = 64;
+}  // namespace
+
+extern "C" int rs16_encode_host_batch(rs16_engine* e, size_t k, size_t m, size_t S, size_t nstripes,
+                                      const void* h_original, size_t original_stride, void* h_recovery,
+                                      size_t recovery_stride, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    if (nstripes == 0) return set_error(err, RS16_OK);
+    if (!h_original || !h_recovery || original_stride < k * S || recovery_stride < m * S)
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    if (int rc = e->activate(err)) return rc;
+    const size_t wc = rs16_encoder_work_count(high, k, m);
+    for (auto& sl : e->hslot) {
+        RS16_HIP(sl.orig.reserve(k * S));
+        RS16_HIP(sl.rec.reserve(m * S));
+    }
+    RS16_HIP(e->ws_z.reserve(wc * S));
+    int urc;
+    uint8_t* U = engine_u(e, high, k, S, err, &urc);
+    if (urc) return urc;
+    if (int rc = e->host_pipe_events(err)) return rc;
+    if (int rc = e->host_slots(err)) return rc;  // (copy streams after the engine stream's earlier work)
+    hipStream_t cin = e->hslot[0].s, cout = e->hslot[1].s, cs = e->stream;
+    auto& ev = e->hp_ev;
+    for (size_t i = 0; i < nstripes; i++) {
+        const int b = (int)(i & 1);
+        uint8_t* d_o = (uint8_t*)e->hslot[b].orig.p;
+        uint8_t* d_r = (uint8_t*)e->hslot[b].rec.p;
+        if (i >= 2) RS16_HIP(hipStreamWaitEvent(cin, ev[HP_CODEC][b], 0));
+        RS16_HIP(hipMemcpyAsync(d_o, (const uint8_t*)h_original + i * original_stride, k * S, hipMemcpyHostToDevice,
+                                cin));
+        RS16_HIP(hipEventRecord(ev[HP_H2D][b], cin));
+        RS16_HIP(hipStreamWaitEvent(cs, ev[HP_H2D][b], 0));
+        if (i >= 2) RS16_HIP(hipStreamWaitEvent(cs, ev[HP_D2H][b], 0));
+        if (int rc = encode_dev(e, high, k, m, S, d_o, d_r, (uint8_t*)e->ws_z.p, U, cs, err)) return rc;
+        RS16_HIP(hipEventRecord(ev[HP_CODEC][b], cs));
+        RS16_HIP(hipStreamWaitEvent(cout, ev[HP_CODEC][b], 0));
+        RS16_HIP(hipMemcpyAsync((uint8_t*)h_recovery + i * recovery_stride, d_r, m * S, hipMemcpyDeviceToHost, cout));
+        RS16_HIP(hipEventRecord(ev[HP_D2H][b], cout));
+    }
+    RS16_HIP(hipStreamSynchronize(cout));
+    RS16_HIP(hipStreamSynchronize(cin));
+    RS16_HIP(hipStreamSynchronize(cs));
+    if (int rc = e->scratch_done(cs, err)) return rc;
+    return set_error(err, RS16_OK);
+}
+
+extern "C" int rs16_decode_host_batch(rs16_engine* e, size_t k, size_t m, size_t S, size_t nstripes,
+                                      void* h_original, size_t original_stride, const uint8_t* original_received,
+                                      size_t original_received_stride, const void* h_recovery,
+                                      size_t recovery_stride, const uint8_t* recovery_received,
+                                      size_t recovery_received_stride, rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    if (nstripes == 0) return set_error(err, RS16_OK);
+    if (!h_original || !h_recovery || !original_received || !recovery_received || original_stride < k * S ||
+        recovery_stride < m * S || original_received_stride < k || recovery_received_stride < m)
+        return set_error(err, RS16_INVALID_ARGUMENT);
+    // every stripe's counts first (src/rate/decoder_work.rs:120-139): a stripe
+    // with too few shards fails the call before anything moves
+    std::vector<size_t> ocnt(nstripes), rcnt(nstripes);
+    for (size_t i = 0; i < nstripes; i++) {
+        const uint8_t* fo = original_received + i * original_received_stride;
+        const uint8_t* fr = recovery_received + i * recovery_received_stride;
+        size_t o = 0, r = 0;
+        for (size_t j = 0; j < k; j++) o += fo[j] != 0;
+        for (size_t j = 0; j < m; j++) r += fr[j] != 0;
+        if (o + r < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, o, r);
+        ocnt[i] = o;
+        rcnt[i] = r;
+    }
+    if (int rc = e->activate(err)) return rc;
+    const DecodeGeom g0 = decode_geom(high, k, m);
+    for (auto& sl : e->hslot) {
+        RS16_HIP(sl.orig.reserve(k * S));
+        RS16_HIP(sl.rec.reserve(m * S));
+    }
+    RS16_HIP(e->ws_z.reserve((size_t)g0.n * S));
+    RS16_HIP(e->ws_u.reserve((size_t)g0.n * S));
+    RS16_HIP(e->hflags.reserve(2 * (k + m)));
+    RS16_HIP(e->hp_flags.reserve(2 * (k + m)));
+    if (int rc = e->host_pipe_events(err)) return rc;
+    if (int rc = e->host_slots(err)) return rc;
+    hipStream_t cin = e->hslot[0].s, cout = e->hslot[1].s, cs = e->stream;
+    auto& ev = e->hp_ev;
+    for (size_t i = 0; i < nstripes; i++) {
+        const int b = (int)(i & 1);
+        uint8_t* d_o = (uint8_t*)e->hslot[b].orig.p;
+        uint8_t* d_r = (uint8_t*)e->hslot[b].rec.p;
+        uint8_t* d_of = (uint8_t*)e->hflags.p + b * (k + m);
+        uint8_t* d_rf = d_of + k;
+        const uint8_t* fo = original_received + i * original_received_stride;
+        const uint8_t* fr = recovery_received + i * recovery_received_stride;
+        uint8_t* ho = (uint8_t*)h_original + i * original_stride;
+        const uint8_t* hr = (const uint8_t*)h_recovery + i * recovery_stride;
+        const bool work = ocnt[i] < k;  // (nothing lost: nothing moves, nothing runs)
+        // ---- in: flags and the received rows (after stripe i - 2's codec
+        // read them and its D2H read the originals restored in place there)
+        if (i >= 2) {
+            RS16_HIP(hipStreamWaitEvent(cin, ev[HP_CODEC][b], 0));
+            RS16_HIP(hipStreamWaitEvent(cin, ev[HP_D2H][b], 0));
+        }
+        if (work) {
+            // the flags go through page-locked staging (a pageable source
+            // would make the copy synchronous and stall the pipeline); the
+            // slot was last read by stripe i - 2's copy
+            uint8_t* hf = (uint8_t*)e->hp_flags.p + b * (k + m);
+            if (i >= 2) RS16_HIP(hipEventSynchronize(ev[HP_H2D][b]));
+            memcpy(hf, fo, k);
+            memcpy(hf + k, fr, m);
+            RS16_HIP(hipMemcpyAsync(d_of, hf, k + m, hipMemcpyHostToDevice, cin));
+            if (int rc = copy_runs(fr, m, true, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
+                    RS16_HIP(hipMemcpyAsync(d_r + r0 * S, hr + r0 * S, nr * S, hipMemcpyHostToDevice, cin));
+                    return RS16_OK;
+                }))
+                return rc;
+            if (int rc = copy_runs(fo, k, true, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
+                    RS16_HIP(hipMemcpyAsync(d_o + r0 * S, ho + r0 * S, nr * S, hipMemcpyHostToDevice, cin));
+                    return RS16_OK;
+                }))
+                return rc;
+        }
+        RS16_HIP(hipEventRecord(ev[HP_H2D][b], cin));
+        // ---- codec
+        RS16_HIP(hipStreamWaitEvent(cs, ev[HP_H2D][b], 0));
+        if (i >= 2) RS16_HIP(hipStreamWaitEvent(cs, ev[HP_D2H][b], 0));
+        if (work) {
+            DecodeGeom g = g0;
+            g.a_recv = high ? rcnt[i] : ocnt[i];
+            g.b_recv = high ? ocnt[i] : rcnt[i];
+            const uint8_t* fa = high ? d_rf : d_of;
+            const uint8_t* fb = high ? d_of : d_rf;
+            if (int rc = e->decode_eval(g, fa, fb, cs, err, S)) return rc;
+            if (int rc = e->decode_passes(g, S, S, high ? d_r : d_o, fa, high ? d_o : d_r, fb, d_o,
+                                          (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, cs,
+                                          err))
+                return rc;
+        }
+        RS16_HIP(hipEventRecord(ev[HP_CODEC][b], cs));
+        // ---- out: the restored originals only
+        RS16_HIP(hipStreamWaitEvent(cout, ev[HP_CODEC][b], 0));
+        if (work)
+            if (int rc = copy_runs(fo, k, false, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
+                    RS16_HIP(hipMemcpyAsync(ho + r0 * S, d_o + r0 * S, nr * S, hipMemcpyDeviceToHost, cout));
+                    return RS16_OK;
+                }))
+                return rc;
+        RS16_HIP(hipEventRecord(ev[HP_D2H][b], cout));
+    }
+    RS16_HIP(hipStreamSynchronize(cout));
+    RS16_HIP(hipStreamSynchronize(cin));
+    RS16_HIP(hipStreamSynchronize(cs));
+    if (int rc = e->scratch_done(cs, err)) return rc;
+    e->forget_decode();  // (the counts came from the host flags: nothing for rs16_decode_check)
+    return set_error(err, RS16_OK);
+}
+
+// ---------------------------------------------------------------------------
 // Several GPUs in one process: the byte columns of one stripe are split over
 // the engines (every 64-byte column block is an independent codeword,
 // src/algorithm.md:18-32); each engine copies its column
@@ -1184,13 +1399,27 @@ extern "C" int rs16_decode_host_multi(rs16_engine* const* engines, int n, size_t
 }
 
 // A decode with nothing to restore (every original received) launches no
-// kernel that counts the flags: remember them, rs16_decode_check reads them.
-static void note_flags_only(rs16_engine* e, const DecodeGeom& g, const uint8_t* fl_a, const uint8_t* fl_b) {
+// kernel that counts the flags: the flags are copied, as they are at the
+// decode's place in stream order, into the engine's ws_flags (segment A at
+// 0, B at GF_ORDER), and rs16_decode_check counts that copy -- the caller may
+// free or reuse its arrays after the call.  A NULL flag array counts as no
+// received rows (the kernels read NULL flags as "none received" too).
+static int note_flags_only(rs16_engine* e, const DecodeGeom& g, const uint8_t* fl_a, const uint8_t* fl_b,
+                           void* stream, rs16_error* err) {
     e->forget_decode();
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
+    RS16_HIP(e->ws_flags.reserve(2 * (size_t)GF_ORDER));
+    uint8_t* f = (uint8_t*)e->ws_flags.p;
+    if (fl_a) RS16_HIP(hipMemcpyAsync(f, fl_a, g.a_count, hipMemcpyDeviceToDevice, s));
+    else RS16_HIP(hipMemsetAsync(f, 0, g.a_count, s));
+    if (fl_b) RS16_HIP(hipMemcpyAsync(f + GF_ORDER, fl_b, g.b_count, hipMemcpyDeviceToDevice, s));
+    else RS16_HIP(hipMemsetAsync(f + GF_ORDER, 0, g.b_count, s));
+    if (int rc = e->scratch_done(s, err)) return rc;
     e->last_dec = g;
-    e->last_flags_a = fl_a;
-    e->last_flags_b = fl_b;
     e->last_dec_flags_only = true;
+    return set_error(err, RS16_OK);
 }
 
 extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, void* d_original,
@@ -1207,7 +1436,7 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     g.b_recv = high ? orig_recv : rec_recv;
     const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
     const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
-    if (orig_recv == k) return note_flags_only(e, g, fl_a, fl_b), set_error(err, RS16_OK);
+    if (orig_recv == k) return note_flags_only(e, g, fl_a, fl_b, stream, err);
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);
     if (int rc = e->order(s, err)) return rc;
@@ -1265,9 +1494,8 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
         DecodeGeom g0 = decode_geom(high, k, m);
         g0.a_recv = high ? rec_recv : orig_recv;
         g0.b_recv = high ? orig_recv : rec_recv;
-        note_flags_only(e, g0, high ? d_recovery_received : d_original_received,
-                        high ? d_original_received : d_recovery_received);
-        return set_error(err, RS16_OK);
+        return note_flags_only(e, g0, high ? d_recovery_received : d_original_received,
+                               high ? d_original_received : d_recovery_received, stream, err);
     }
     if (!d_original || !d_recovery || original_stride < k * S || recovery_stride < m * S || original_stride % 64 ||
         recovery_stride % 64 || nstripes > ((size_t)1 << 20))
@@ -1303,9 +1531,11 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
 // in the host arrays.  One launch of the eval kernels with a grid row per
 // stripe (per-stripe erasure logs, received bitmaps, zero tiles, lost
 // ranges), then the pass launches shared by all stripes, each workgroup
-// reading its stripe's metadata.  Path: the half-transform decode when no
-// stripe received an original, else the general decode for all; the
-// first-pass tiles launched are the union over the stripes.
+// reading its stripe's metadata.  Stripes go in groups of at most 256 (the
+// scratch is sized for one group).  Path, per group: the half-transform
+// decode when no stripe of it received an original, else the general decode
+// for all of them; the first-pass tiles launched are the union over the
+// group's stripes.
 extern "C" int rs16_decode_device_batch_varied(rs16_engine* e, size_t k, size_t m, size_t S, size_t nstripes,
                                                void* d_original, size_t original_stride,
                                                const uint8_t* d_original_received, size_t original_received_stride,
@@ -1322,41 +1552,50 @@ extern "C" int rs16_decode_device_batch_varied(rs16_engine* e, size_t k, size_t 
         recovery_stride % 64 || original_received_stride < k || recovery_received_stride < m ||
         nstripes > ((size_t)1 << 16))
         return set_error(err, RS16_INVALID_ARGUMENT);
-    size_t max_o = 0, max_r = 0;
-    bool any_lost = false;
     for (size_t i = 0; i < nstripes; i++) {
         const size_t o = original_received_counts[i], r = recovery_received_counts[i];
         if (o > k || r > m) return set_error(err, RS16_INVALID_ARGUMENT);
         if (o + r < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, o, r);  // (the first such stripe)
-        max_o = std::max(max_o, o);
-        max_r = std::max(max_r, r);
-        any_lost |= o < k;
     }
-    if (!any_lost) return set_error(err, RS16_OK);  // nothing to restore in any stripe
     if (int rc = e->activate(err)) return rc;
     hipStream_t s = e->pick(stream);
     if (int rc = e->order(s, err)) return rc;
-    DecodeGeom g = decode_geom(high, k, m);
-    // (a segment counts as received when any stripe received a shard of it)
-    g.a_recv = high ? max_r : max_o;
-    g.b_recv = high ? max_o : max_r;
-    RS16_HIP(e->ws_z.reserve(nstripes * g.n * S));
-    RS16_HIP(e->ws_u.reserve(nstripes * g.n * S));
-    const uint8_t* orig = (const uint8_t*)d_original;
     const uint8_t* rec = (const uint8_t*)d_recovery;
-    const uint8_t* seg_a = high ? rec : orig;
-    const uint8_t* seg_b = high ? orig : rec;
     const size_t bs_a = high ? recovery_stride : original_stride, bs_b = high ? original_stride : recovery_stride;
-    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
-    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
     const size_t fs_a = high ? recovery_received_stride : original_received_stride;
     const size_t fs_b = high ? original_received_stride : recovery_received_stride;
-    const uint32_t vary = nstripes > 1 ? (uint32_t)nstripes : 0;
-    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, S, nstripes, vary, fs_a, fs_b)) return rc;
-    if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
-                                  (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, s, err, nstripes, bs_a, bs_b,
-                                  original_stride))
-        return rc;
+    // Groups of at most VARY_GROUP stripes: the per-stripe metadata (erasure
+    // logs, received bitmaps, ... 0.5 MiB a stripe) and the work rows (2 n S
+    // bytes a stripe) are reserved for one group, not for the whole call.
+    constexpr size_t VARY_GROUP = 256;
+    for (size_t g0 = 0; g0 < nstripes; g0 += VARY_GROUP) {
+        const size_t ns = std::min(VARY_GROUP, nstripes - g0);
+        size_t max_o = 0, max_r = 0;
+        bool any_lost = false;
+        for (size_t i = g0; i < g0 + ns; i++) {
+            max_o = std::max(max_o, original_received_counts[i]);
+            max_r = std::max(max_r, recovery_received_counts[i]);
+            any_lost |= original_received_counts[i] < k;
+        }
+        if (!any_lost) continue;  // nothing to restore in any stripe of the group
+        DecodeGeom g = decode_geom(high, k, m);
+        // (a segment counts as received when any stripe received a shard of it)
+        g.a_recv = high ? max_r : max_o;
+        g.b_recv = high ? max_o : max_r;
+        RS16_HIP(e->ws_z.reserve(ns * g.n * S));
+        RS16_HIP(e->ws_u.reserve(ns * g.n * S));
+        uint8_t* og = (uint8_t*)d_original + g0 * original_stride;
+        const uint8_t* rg = rec + g0 * recovery_stride;
+        const uint8_t* seg_a = high ? rg : og;
+        const uint8_t* seg_b = high ? og : rg;
+        const uint8_t* fl_a = (high ? d_recovery_received : d_original_received) + g0 * fs_a;
+        const uint8_t* fl_b = (high ? d_original_received : d_recovery_received) + g0 * fs_b;
+        const uint32_t vary = ns > 1 ? (uint32_t)ns : 0;
+        if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, S, ns, vary, fs_a, fs_b)) return rc;
+        if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, og, (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p,
+                                      (uint32_t*)e->ws_rcount.p, s, err, ns, bs_a, bs_b, original_stride))
+            return rc;
+    }
     e->forget_decode();
     if (int rc = e->scratch_done(s, err)) return rc;
     return set_error(err, RS16_OK);

@@ -49,6 +49,7 @@
 #include "rs16_internal.hpp"
 #include "rs16_fwht.hpp"
 #include "rs16_colops.hpp"
+#include "rs16_diag.hpp"
 
 namespace rs16 {
 
@@ -139,29 +140,6 @@ __device__ __forceinline__ void exchange(uint32_t (&XL)[4], uint32_t (&XH)[4], u
     }
 }
 
-// Diagnostic timeline (-DRS16_STAMPS=1 builds only, scripts/stamps.py):
-// thread 0 stores s_memtime at phase i to stamps[block * 16 + i] (14 / 15:
-// s_memrealtime at start / end, 12 / 13: HW_ID / XCC_ID).
-#ifndef RS16_STAMPS
-#define RS16_STAMPS 0
-#endif
-__device__ __forceinline__ void cstamp(const ColArgs& a, int i) {
-#if RS16_STAMPS
-    if (a.stamps && threadIdx.x == 0) {
-        uint64_t* p = a.stamps + blockIdx.x * 16;
-        p[i] = __builtin_amdgcn_s_memtime();
-        if (i == 0) {
-            p[14] = __builtin_amdgcn_s_memrealtime();
-            p[12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            p[13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-        }
-        if (i == 11) p[15] = __builtin_amdgcn_s_memrealtime();
-    }
-#else
-    (void)a;
-    (void)i;
-#endif
-}
 
 // ---------------------------------------------------------------------------
 // eval_poly inside the decoder (COL_DEC_EVAL, high rate, n = 2N <= 2048 work
@@ -346,7 +324,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     constexpr int N = 1 << L, NT = N / 4;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t t = threadIdx.x;
-    cstamp(a, 0);
+    RS16_STAMP(a, 0);
 
     // workgroup -> (stripe, quad column), XCD-aware: consecutive columns on
     // one XCD (workgroups are dealt to the 8 XCDs round-robin)
@@ -470,7 +448,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         // multiply below waits for both)
         dma_tables();
     }
-    cstamp(a, 1);
+    RS16_STAMP(a, 1);
     if constexpr (DEC) {
 #pragma unroll
         for (int m = 0; m < 4; m++) {
@@ -484,7 +462,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads have landed)
         __syncthreads();
     }
-    cstamp(a, 2);
+    RS16_STAMP(a, 2);
 
     // ---- IFFT (layers 0 .. L-1) then FFT (L-1 .. 0) in radix-4 blocks; the
     // next block's tables are read before each exchange.  Row bits 0-5 are
@@ -498,14 +476,14 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     static_assert(GEN, "2^11 rows: the general decoder only");
     load_tabs01_img<L>(ta, t, a.img_ifft);
     compute<false, true, true>(XL, XH, ta);
-    cstamp(a, 3);
+    RS16_STAMP(a, 3);
     load_tabs<L, false, 2, 3, true, true>(tb, t, smem);
     wave_exchange<0, 1>(XL, XH);
     compute<false, true, true>(XL, XH, tb);
     load_tabs<L, false, 4, 5, true, true>(ta, t, smem);
     wave_exchange<2, 3>(XL, XH);
     compute<false, true, true>(XL, XH, ta);
-    cstamp(a, 4);
+    RS16_STAMP(a, 4);
     load_tabs<L, false, 6, 7, true, true>(tb, t, smem);
     wave_exchange<4, 5>(XL, XH);
     compute<false, true, true>(XL, XH, tb);
@@ -516,7 +494,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     __syncthreads();  // (every wave has read its rows of the image)
     exchange<8, 9, 8, 10>(XL, XH, t, smem);
     compute<false, false, true>(XL, XH, tb);
-    cstamp(a, 5);
+    RS16_STAMP(a, 5);
     col_fd<L, 8, 10>(XL, XH, t, smem);
     load_tabs<L, true, 8, 10, false, true>(tb, t, smem);
     compute<true, false, true>(XL, XH, tb);
@@ -524,7 +502,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     __syncthreads();
     exchange<8, 10, 8, 9>(XL, XH, t, smem);
     compute<true, true, true>(XL, XH, ta);
-    cstamp(a, 6);
+    RS16_STAMP(a, 6);
     load_tabs<L, true, 6, 7, true, true>(tb, t, smem);
     __syncthreads();
     exchange<8, 9, 6, 7>(XL, XH, t, smem);
@@ -532,57 +510,57 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
     load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
     wave_exchange<4, 5>(XL, XH);
     compute<true, true, true>(XL, XH, ta);
-    cstamp(a, 7);
+    RS16_STAMP(a, 7);
     load_tabs<L, true, 2, 3, true, true>(tb, t, smem);
     wave_exchange<2, 3>(XL, XH);
     compute<true, true, true>(XL, XH, tb);
     load_tabs01_img<L>(tb, t, a.img_fft);
     wave_exchange<0, 1>(XL, XH);
-    cstamp(a, 8);
+    RS16_STAMP(a, 8);
   } else {
     compute<false, true, true>(XL, XH, ta);  // (layers 0, 1: tables from registers)
     __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
     __syncthreads();
-    cstamp(a, 3);
+    RS16_STAMP(a, 3);
     load_tabs<L, false, 2, 3, true, true>(tb, t, smem);
     wave_exchange<0, 1>(XL, XH);
     compute<false, true, true>(XL, XH, tb);
     load_tabs<L, false, 4, 5, true, true>(ta, t, smem);
     wave_exchange<2, 3>(XL, XH);
     compute<false, true, true>(XL, XH, ta);
-    cstamp(a, 4);
+    RS16_STAMP(a, 4);
     if constexpr (L == 6) {
         // the FFT's first block keeps the row bits (4, 5)
-        cstamp(a, 5);
+        RS16_STAMP(a, 5);
         if constexpr (GEN) col_fd<L, 4, 5>(XL, XH, t, smem);
         load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
-        cstamp(a, 6);
+        RS16_STAMP(a, 6);
     } else if constexpr (L == 7) {
         load_tabs<L, false, 4, 6, false, true>(tb, t, smem);
         swap_bit<1, 4>(XL);  // register bit 1: row bit 5 -> 6
         swap_bit<1, 4>(XH);
         compute<false, false, true>(XL, XH, tb);
-        cstamp(a, 5);
+        RS16_STAMP(a, 5);
         if constexpr (GEN) col_fd<L, 4, 6>(XL, XH, t, smem);
         load_tabs<L, true, 4, 6, false, true>(tb, t, smem);
         compute<true, false, true>(XL, XH, tb);
         load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
         swap_bit<1, 4>(XL);
         swap_bit<1, 4>(XH);
-        cstamp(a, 6);
+        RS16_STAMP(a, 6);
     } else {
         load_tabs<L, false, 6, 7, true, true>(tb, t, smem);
         wave_exchange<4, 5>(XL, XH);
         compute<false, true, true>(XL, XH, tb);
         if constexpr (L == 8) {
-            cstamp(a, 5);
+            RS16_STAMP(a, 5);
             if constexpr (GEN) col_fd<L, 6, 7>(XL, XH, t, smem);
             load_tabs<L, true, 6, 7, true, true>(ta, t, smem);
         } else if constexpr (L == 10) {
             load_tabs<L, false, 8, 9, true, true>(ta, t, smem);
             exchange<6, 7, 8, 9>(XL, XH, t, smem);
             compute<false, true, true>(XL, XH, ta);
-            cstamp(a, 5);
+            RS16_STAMP(a, 5);
             if constexpr (GEN) col_fd<L, 8, 9>(XL, XH, t, smem);
             // the FFT's first block keeps the row bits: no exchange
             load_tabs<L, true, 8, 9, true, true>(tb, t, smem);
@@ -594,7 +572,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             load_tabs<L, false, 7, 8, false, true>(ta, t, smem);
             exchange<6, 7, 7, 8>(XL, XH, t, smem);
             compute<false, false, true>(XL, XH, ta);
-            cstamp(a, 5);
+            RS16_STAMP(a, 5);
             if constexpr (GEN) col_fd<L, 7, 8>(XL, XH, t, smem);
             load_tabs<L, true, 7, 8, false, true>(tb, t, smem);
             compute<true, false, true>(XL, XH, tb);
@@ -602,19 +580,19 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             __syncthreads();  // (every wave has read its rows of the image)
             exchange<7, 8, 6, 7>(XL, XH, t, smem);
         }
-        cstamp(a, 6);
+        RS16_STAMP(a, 6);
         compute<true, true, true>(XL, XH, ta);
         load_tabs<L, true, 4, 5, true, true>(ta, t, smem);
         wave_exchange<4, 5>(XL, XH);
     }
     compute<true, true, true>(XL, XH, ta);
-    cstamp(a, 7);
+    RS16_STAMP(a, 7);
     load_tabs<L, true, 2, 3, true, true>(tb, t, smem);
     wave_exchange<2, 3>(XL, XH);
     compute<true, true, true>(XL, XH, tb);
     tb = t01f;  // (layers 1, 0: tables from registers)
     wave_exchange<0, 1>(XL, XH);
-    cstamp(a, 8);
+    RS16_STAMP(a, 8);
   }
     uint32_t rt[DEC ? 4 : 1][20];
     if constexpr (DEC) {
@@ -624,7 +602,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
         for (int m = 0; m < 4; m++) glb_table(rt[m], a.mul_tab, GF_MODULUS - ev[m]);
     }
     compute<true, true, true>(XL, XH, tb);
-    cstamp(a, 9);
+    RS16_STAMP(a, 9);
 
     // ---- store rows 4t + m < out_rows (DEC: revealed, rate_high.rs:236-242)
 #pragma unroll
@@ -644,11 +622,8 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
             __builtin_nontemporal_store(vh, p + 8);
         }
     }
-    cstamp(a, 10);
-#if RS16_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    cstamp(a, 11);
-#endif
+    RS16_STAMP(a, 10);
+    RS16_STAMP_END(a);
 }
 
 
@@ -815,7 +790,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     using FM = typename SMap<L, L - 1>::M;  // the rows' map between the IFFT's last layer and the FFT's first
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t t = threadIdx.x;
-    cstamp(a, 0);
+    RS16_STAMP(a, 0);
 
     const uint32_t total = a.qrow * a.nstripes;
     uint32_t g = blockIdx.x;
@@ -949,7 +924,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
             XH[m] = zh;
         }
     }
-    cstamp(a, 1);
+    RS16_STAMP(a, 1);
     // Each layer's LDS table is read one layer ahead (wa / wb), so its
     // latency hides under the previous layer's swap and butterfly.
     uint8_t* img = smem + ColSmem<L>::IMG;
@@ -966,7 +941,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     bfly2<false>(XL, XH, i0);
     __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
     __syncthreads();
-    cstamp(a, 2);
+    RS16_STAMP(a, 2);
     if constexpr (L <= 10 && !IFO) {
         tab2_img<L, 0, S0>(f0, t, img_fft);
         tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, img_fft);
@@ -989,7 +964,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     tab2<L, false, 7, MM>(wb, t, smem);
     swap2<5>(XL, XH);
     bfly2<false>(XL, XH, wa);
-    cstamp(a, 3);
+    RS16_STAMP(a, 3);
     }
     // ---- layers 7 .. L-1 both ways around the middle, map M (GEN: the
     // formal derivative between the IFFT's last layer and the FFT's first)
@@ -1095,7 +1070,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         bfly2<true>(XL, XH, wa);   // FFT 7
         if constexpr (GEN) __syncthreads();
     }
-    cstamp(a, 4);
+    RS16_STAMP(a, 4);
     tab2<L, true, 5, S5>(wa, t, smem);
     // (each thread writes the image rows it read in the first exchange: no
     // barrier; GEN: the derivative's image reads are behind a barrier above)
@@ -1121,7 +1096,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     }
     swap2<0>(XL, XH);
     bfly2<true>(XL, XH, f0);
-    cstamp(a, 9);
+    RS16_STAMP(a, 9);
     // ---- store rows < out_rows (DEC: revealed, rate_high.rs:236-242; GEN:
     // the lost originals only, restored in place)
 #pragma unroll
@@ -1143,11 +1118,8 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
             p[8] = vh;
         }
     }
-    cstamp(a, 10);
-#if RS16_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    cstamp(a, 11);
-#endif
+    RS16_STAMP(a, 10);
+    RS16_STAMP_END(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1272,6 +1244,11 @@ __global__ __launch_bounds__(1024) void colm_kernel(ColArgs a) {
                 XH[m] ^= v.y;
             }
         }
+    } else {
+        // every wave has consumed its loaded originals (the IFFT used them)
+        // before wave 0 stores recovery rows [0, 128): the Rate API encodes
+        // in place, recovery over the originals (rate_low.rs:44-83)
+        __syncthreads();
     }
     // ---- FFT layers 6 .. 0
     cm_tab<6, S6>(wa, lane, tF);
@@ -1313,12 +1290,17 @@ hipError_t launch_col_multi(const ColArgs& a, bool high, hipStream_t s) {
     if (a.qrow == 0 || a.nstripes == 0 || a.out_rows == 0) return hipSuccess;
     const int bytes = (int)(a.nch * 2 * CM_TAB_BYTES + (high ? a.nch * CM_N * 8 : 0));
     const auto fn = high ? colm_kernel<true> : colm_kernel<false>;
-    static bool attr[2] = {false, false};  // (idempotent: a racing second call sets it again)
-    if (!attr[high]) {
+    // the LDS limit is a per-device attribute: set it for the current device
+    // the first time this process launches there (engines on several GPUs)
+    constexpr int MAX_DEV = 64;
+    static bool attr[MAX_DEV][2] = {};  // (idempotent: a racing second call sets it again)
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    if (dev < 0 || dev >= MAX_DEV || !attr[dev][high]) {
         const int most = (int)(COLM_MAX_CHUNKS * 2 * CM_TAB_BYTES + COLM_MAX_CHUNKS * CM_N * 8);
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, most);
         if (e != hipSuccess) return e;
-        attr[high] = true;
+        if (dev >= 0 && dev < MAX_DEV) attr[dev][high] = true;
     }
     hipLaunchKernelGGL(fn, dim3(a.qrow * a.nstripes), dim3(64 * a.nch), bytes, s, a);
     return hipGetLastError();
@@ -1352,7 +1334,7 @@ hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s) {
         fn = fnc[L - COL_LCHUNK][mode == COL_ENC ? 0 : mode - COL_ENC_IFFT + 1];
         threads = (1u << L) / 2;
         rows = mode == COL_ENC_FFTX ? 1 : a.nch;  // (one grid row per chunk)
-    } else if (mode != COL_DEC_EWORK && L >= 8 && !(g_diag & DIAG_COL_RADIX4)) {
+    } else if (mode != COL_DEC_EWORK && L >= 8 && !(a.diag & DIAG_COL_RADIX4)) {
         // the encode and the half decode of 2^8 .. 2^10 rows: the radix-2
         // form (2 rows per thread), unless RS16_DIAG_COL_RADIX4
         static const ColFn fns2[4][3] = {

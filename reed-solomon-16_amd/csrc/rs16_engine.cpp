@@ -8,8 +8,6 @@
 
 namespace rs16 {
 
-int g_diag = 0;
-
 hipError_t DevBuf::reserve(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipFree(p);
@@ -95,6 +93,7 @@ static PassArgs base_args(const rs16_engine* e, size_t S) {
     a.zero = e->d_zero_sink;
     a.S_in = a.S_out = a.S_seg = a.S_rest = S;
     a.qrow = (uint32_t)(S / 8);
+    a.diag = (uint32_t)e->diag;
     return a;
 }
 
@@ -216,8 +215,8 @@ int rs16_engine::pass(int prog, int T, const PassArgs& a, uint32_t tiles, hipStr
 
 bool rs16_engine::col_ok(int L, size_t S, size_t nstripes, bool gen) const {
     const bool rows = col_rows_ok((uint32_t)L) || (gen && L == (int)COL_LGEN);
-    if (!rows || (g_diag & DIAG_NO_COLUMN)) return false;
-    return (S / 8) * nstripes <= col_max_quads || (g_diag & DIAG_FORCE_COLUMN);
+    if (!rows || (diag & DIAG_NO_COLUMN)) return false;
+    return (S / 8) * nstripes <= col_max_quads || (diag & DIAG_FORCE_COLUMN);
 }
 
 // the radix-2 multi-chunk encodes (launch_col, COL_ENC_IFFT / COL_ENC_FFTX /
@@ -228,7 +227,7 @@ bool rs16_engine::col_ok(int L, size_t S, size_t nstripes, bool gen) const {
 bool rs16_engine::col_chunks_ok(int L, uint32_t nch, size_t S, bool high) const {
     const size_t rows_max = high && L <= 9 ? std::max<size_t>(col_max_chunk_rows, 8192) : col_max_chunk_rows;
     return L >= (int)COL_LCHUNK && L <= (int)COL_LMAX && nch > 1 && nch <= COL_MAX_CHUNKS &&
-           (((size_t)nch << L) <= rows_max || (g_diag & DIAG_FORCE_COLUMN)) &&
+           (((size_t)nch << L) <= rows_max || (diag & DIAG_FORCE_COLUMN)) &&
            nch < col_img_count((uint32_t)L) && col_ok(L, S, 1);
 }
 
@@ -240,6 +239,7 @@ ColArgs rs16_engine::col_args() const {
     a.zero = d_zero_sink;
     a.elog = (const uint32_t*)ws_elog.p;
     a.nstripes = 1;
+    a.diag = (uint32_t)diag;
     return a;
 }
 
@@ -470,6 +470,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     es.lostrange = prune ? (uint32_t*)ws_lost.p + 512 : nullptr;
     es.orig_b = g.high ? 1 : 0;
     es.rcount = (uint32_t*)ws_rcount.p;
+    es.diag = (uint32_t)diag;
     last_dec = g;
     last_dec_valid = true;
     if (var_ns) {
@@ -498,7 +499,7 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // 256-point FWHT themselves, for the 256-row block of their tile's rows
     // (one kernel less) -- except the one-pass half-transform decode, whose
     // gather and reveal rows lie in different blocks.
-    const bool small = g.high && g.n <= 2048 && !(g_diag & DIAG_EVAL_FULL);
+    const bool small = g.high && g.n <= 2048 && !(diag & DIAG_EVAL_FULL);
     // (the column codec's half decodes of 2^9 / 2^10 rows finish it too)
     elog_fused = !(half_decode(g) && ilog2(g.n) - 1 <= 8);
     if (small) {
@@ -709,7 +710,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     // this pass): one wave per quad column of each tile (tile_last_kernel)
     // instead of one 8-wave item per 32 quads, whose latency was the pass.
     const size_t lost = g.high ? (size_t)g.b_count - g.b_recv : (size_t)g.a_count - g.a_recv;
-    const bool tile_last = lo == 8 && !(g_diag & DIAG_NO_TILE_LAST) && (lost <= 2048 || (g_diag & DIAG_TILE_LAST));
+    const bool tile_last = lo == 8 && !(diag & DIAG_NO_TILE_LAST) && (lost <= 2048 || (diag & DIAG_TILE_LAST));
     if (tile_last) {
         const uint32_t tiles = batch(t1 - t0, zs, zs, 0);
         hipEvent_t ev;
@@ -846,11 +847,27 @@ int rs16_engine::encode_low_multi(size_t k, size_t m, size_t S, size_t S_user, c
         return col_multi(k, m, S, S_user, d_orig, d_rec, nch, false, s, err);
     if (nch > 1 && col_chunks_ok(L, nch, S, false)) {
         // 256 / 512 / 1024-row chunks: one launch, one workgroup per (quad
-        // column, recovery chunk), each running the originals' IFFT itself
+        // column, recovery chunk), each running the originals' IFFT itself.
+        // Every chunk's workgroups read the originals, and chunk 0's write
+        // recovery rows [0, chunk): when the two arrays overlap (the Rate
+        // API's work buffer, rate_low.rs:44-83) chunk 0 could overwrite
+        // originals other chunks have not loaded yet, so the originals are
+        // read from a copy in U then (U: next_pow2(k) rows, pitch S).
+        const uint8_t* src = d_orig;
+        size_t s_in = S_user;
+        const uint8_t *o0 = d_orig, *o1 = d_orig + (k - 1) * S_user + S;
+        const uint8_t *r0 = d_rec, *r1 = d_rec + (m - 1) * S_user + S;
+        if (o0 < r1 && r0 < o1) {
+            if (!U) return set_error(err, RS16_INVALID_ARGUMENT);
+            RS16_HIP(hipMemcpy2DAsync(U, S, d_orig, S_user, S, k, hipMemcpyDeviceToDevice, s));
+            src = U;
+            s_in = S;
+        }
         ColArgs c = col_args();
-        c.in = d_orig;
+        c.in = src;
         c.out = d_rec;
-        c.S_in = c.S_out = S_user;
+        c.S_in = s_in;
+        c.S_out = S_user;
         c.qrow = (uint32_t)(S / 8);
         c.in_rows = (uint32_t)k;
         c.out_rows = (uint32_t)m;

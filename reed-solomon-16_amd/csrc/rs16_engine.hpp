@@ -72,6 +72,8 @@ struct rs16_decoder;
 struct rs16_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    // diagnostic switches of this engine (rs16::DiagFlags, rs16_engine_set_diagnostics)
+    int diag = 0;
     uint32_t* d_skew_tab = nullptr;  // v_perm table per twiddle index (8 MiB)
     uint32_t* d_mul_tab = nullptr;
     uint32_t* d_col_img = nullptr;   // column codec table images (HostTables::col_img)
@@ -88,10 +90,8 @@ struct rs16_engine {
     rs16::DecodeGeom last_dec{};
     bool last_dec_valid = false;
     // ... or, when that decode had nothing to restore (every original
-    // received: no kernel counted anything), its device flag arrays, which
-    // rs16_decode_check then reads back and counts itself
-    const uint8_t* last_flags_a = nullptr;
-    const uint8_t* last_flags_b = nullptr;
+    // received: no kernel counted anything), a copy of its flags in ws_flags
+    // (segment A at 0, B at GF_ORDER), which rs16_decode_check counts itself
     bool last_dec_flags_only = false;
     void forget_decode() { last_dec_valid = last_dec_flags_only = false; }
     // Host-resident pipeline (rs16_encode_host / rs16_decode_host): column
@@ -123,6 +123,11 @@ struct rs16_engine {
     int join(hipStream_t s, int n, rs16_error* err);
     rs16::DevBuf hflags;
     hipEvent_t hev = nullptr;
+    // pipelined host stripes (rs16_{en,de}code_host_batch): per buffer parity,
+    // H2D done / codec done / D2H done
+    hipEvent_t hp_ev[3][2] = {};
+    rs16::HostBuf hp_flags;  // page-locked staging of the decode's flag bytes (2 x (k + m))
+    int host_pipe_events(rs16_error* err);
     int host_slots(rs16_error* err);
 
     hipStream_t pick(void* s) const { return s ? (hipStream_t)s : stream; }

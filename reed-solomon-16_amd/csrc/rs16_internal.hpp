@@ -176,6 +176,8 @@ struct PassArgs {
     // bs_lost words (ErasureSpec's per-stripe outputs).  All 0: shared.
     uint64_t bs_fa, bs_fb;
     uint32_t bs_elog, bs_rbits, bs_zflags, bs_lost;
+    // the engine's diagnostic switches (DiagFlags; host side: launch_pass)
+    uint32_t diag;
 };
 
 // One-launch codec for 2^9 / 2^10-row transforms (rs16_col.hip): one
@@ -226,6 +228,7 @@ struct ColArgs {
     uint32_t bs_elog;
     uint32_t nch;               // launch_col_multi: chunks of 128 rows (one wave each); launch_col: chunks (ColMode)
     uint64_t* stamps;           // RS16_STAMPS builds: phase timeline (rs16_engine_set_stamps)
+    uint32_t diag;              // the engine's diagnostic switches (DiagFlags; host side: launch_col)
 };
 int col_rows_ok(uint32_t L);  // L = log2(rows of the transform) the codec covers
 // COL_DEC_GEN: the general high-rate decode of a 2^L-row work buffer (any
@@ -246,9 +249,11 @@ hipError_t launch_col(const ColArgs& a, uint32_t L, int mode, hipStream_t s);
 constexpr uint32_t COLM_L = 7, COLM_MAX_CHUNKS = 16;
 hipError_t launch_col_multi(const ColArgs& a, bool high, hipStream_t s);
 
-// Process-wide diagnostic switches (rs16_set_diagnostics, include/rs16.h):
+// Per-engine diagnostic switches (rs16_engine_set_diagnostics, include/rs16.h):
 // alternative code paths kept for tests and measurements, never needed for
-// correct results.  0 = the shipped behaviour.
+// correct results.  0 = the shipped behaviour.  They travel with the launch
+// arguments (PassArgs / ColArgs / ErasureSpec::diag); there is no process-wide
+// state.
 enum DiagFlags : int {
     DIAG_FORCE_VOFF64 = 1,    // 64-bit lane offsets in every pass (PassArgs::voff32 = 0)
     DIAG_EVAL_TWO_KERNEL = 2, // eval_poly: two-kernel form even when the one-kernel form applies
@@ -260,7 +265,6 @@ enum DiagFlags : int {
     DIAG_FD_LDS = 128,        // DEC_MID's in-tile formal derivative always through the LDS image (tile_fd)
     DIAG_COL_RADIX4 = 256,    // column codec: the 4-rows-per-thread form for every transform (col_kernel)
 };
-extern int g_diag;
 
 constexpr size_t RS16_ZERO_BYTES = 65536;
 
@@ -314,6 +318,7 @@ struct ErasureSpec {           // builds the erasure vector of rate_{high,low}.r
     uint32_t nstripes;
     uint64_t bs_fa, bs_fb;
     uint32_t bs_work, bs_elog, bs_rbits, bs_zflags, bs_lost;
+    uint32_t diag;             // the engine's diagnostic switches (DiagFlags; host side)
 };
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo);

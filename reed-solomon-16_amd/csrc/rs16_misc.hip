@@ -6,6 +6,7 @@
 
 #include "rs16_internal.hpp"
 #include "rs16_fwht.hpp"
+#include "rs16_diag.hpp"
 
 namespace rs16 {
 
@@ -347,34 +348,13 @@ __device__ __forceinline__ int block_region(const ErasureSpec& e, uint32_t base)
     if (base - e.chunk < e.b_count) return 2;
     return 3;
 }
-#ifndef RS16_STAMPS
-#define RS16_STAMPS 0
-#endif
-// (RS16_STAMPS builds: slots as rs16_pass.hip's stamp(), 0 start, 1 flags
-// in, 2 sums done, 10 store issued, 11 store done, 14 / 15 real time)
-__device__ __forceinline__ void estamp(const ErasureSpec& e, int i) {
-#if RS16_STAMPS
-    if (e.stamps && threadIdx.x == 0) {
-        e.stamps[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
-        if (i == 0) {
-            e.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
-            e.stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            e.stamps[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-        }
-        if (i == 11) e.stamps[blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memrealtime();
-    }
-#else
-    (void)e;
-    (void)i;
-#endif
-}
 __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t* out32, const uint16_t* log_walsh) {
     __shared__ int xs[256];
     __shared__ uint32_t lr[2][4];
     const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     stripe_spec(e);
     out32 += blockIdx.y * e.bs_work;
-    estamp(e, 0);
+    RS16_STAMP(e, 0);
     uint32_t lw[4];
     if (wv == 0) {
 #pragma unroll
@@ -432,7 +412,7 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
             }
         }
     }
-    estamp(e, 1);
+    RS16_STAMP(e, 1);
     xs[t] = (j == 0 ? 256 * all : 0) + (acc >> 7);
     if (j == 0 && e.lostrange) {
 #pragma unroll
@@ -461,7 +441,7 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
         e.lostrange[1] = max(max(lr[1][0], lr[1][1]), max(lr[1][2], lr[1][3]));
     }
     if (wv != 0) return;
-    estamp(e, 2);
+    RS16_STAMP(e, 2);
     // ---- wave 0: y = H_hi(x) exactly, w = y * LW mod 65535, z = H_hi(w) ----
     int y[4];
 #pragma unroll
@@ -491,15 +471,12 @@ __global__ void __launch_bounds__(256) eval_fused_kernel(ErasureSpec e, uint32_t
         p = (p & 0xFFFFu) + (p >> 16);
         v[i] = (p & 0xFFFFu) + (p >> 16);
     }
-    estamp(e, 3);
+    RS16_STAMP(e, 3);
     fwht256_wave(v);
-    estamp(e, 10);
+    RS16_STAMP(e, 10);
 #pragma unroll
     for (int i = 0; i < 4; i++) out32[(lane + 64u * i) * 256u + j] = v[i];
-#if RS16_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
-    estamp(e, 11);
+    RS16_STAMP_END(e);
 }
 // Segment boundaries on 256-row blocks and 16-byte aligned flag arrays.
 static bool eval_fused_ok(const ErasureSpec& e) {
@@ -510,7 +487,7 @@ static bool eval_fused_ok(const ErasureSpec& e) {
 hipError_t launch_eval_poly_from_flags(const ErasureSpec& e, uint32_t* work, uint32_t* out_elog,
                                        const uint16_t* log_walsh, hipStream_t s, bool last_lo) {
     const uint32_t ns = e.nstripes > 1 ? e.nstripes : 1;
-    if (!(g_diag & DIAG_EVAL_TWO_KERNEL) && eval_fused_ok(e) && (ns == 1 || (e.bs_fa % 16 == 0 && e.bs_fb % 16 == 0))) {
+    if (!(e.diag & DIAG_EVAL_TWO_KERNEL) && eval_fused_ok(e) && (ns == 1 || (e.bs_fa % 16 == 0 && e.bs_fb % 16 == 0))) {
         hipLaunchKernelGGL(eval_fused_kernel, dim3(256, ns), dim3(256), 0, s, e, work, log_walsh);
     } else {
         hipLaunchKernelGGL(fwht_lo_flags_kernel, dim3(256, ns), dim3(64), 0, s, e, work);
@@ -554,7 +531,7 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
     const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     stripe_spec(e);
     z += blockIdx.y * e.bs_work;
-    estamp(e, 0);
+    RS16_STAMP(e, 0);
     const uint32_t lw = log_walsh[t * 256u + j];  // in flight from the start
     // flag bytes of rows 256 h' + t, all loads issued before the first use
     // (a row outside both segments reads a valid dummy byte)
@@ -605,7 +582,7 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
         lpart[0][wv] = wlo;
         lpart[1][wv] = whi;
     }
-    estamp(e, 1);
+    RS16_STAMP(e, 1);
     __syncthreads();
     if (j == 0 && t == 0 && e.lostrange) {
         e.lostrange[0] = min(min(lpart[0][0], lpart[0][1]), min(lpart[0][2], lpart[0][3]));
@@ -638,14 +615,11 @@ __global__ void __launch_bounds__(256) eval_small_kernel(ErasureSpec e, const ui
         s = (lane & d) ? p - s : s + p;
     }
     if (lane < NB) part[1][wv][lane] = s;
-    estamp(e, 2);
+    RS16_STAMP(e, 2);
     __syncthreads();
     if (t < NB) z[t * 256u + j] = mod65535(part[1][0][t] + part[1][1][t] + part[1][2][t] + part[1][3][t]);
-    estamp(e, 10);
-#if RS16_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    estamp(e, 11);
-#endif
+    RS16_STAMP(e, 10);
+    RS16_STAMP_END(e);
 }
 
 hipError_t launch_eval_poly_small(const ErasureSpec& e, uint32_t n, uint32_t* work, uint32_t* out_elog,

@@ -58,6 +58,7 @@
 #include "rs16_internal.hpp"
 #include "rs16_fwht.hpp"
 #include "rs16_colops.hpp"
+#include "rs16_diag.hpp"
 
 namespace rs16 {
 
@@ -205,14 +206,6 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
     return ur < lim && lr < lim - ur;
 }
 
-// Diagnostic timeline build (-DRS16_STAMPS=1, never the shipped library):
-// wave 0 of every workgroup stores s_memtime at phase boundaries to
-// stamps[block * 16 + phase] (phase 15: s_memrealtime at the end, 14 at
-// the start, for the clock; 12 / 13 the HW_ID / XCC_ID registers).
-// scripts/stamps.py reads them.
-#ifndef RS16_STAMPS
-#define RS16_STAMPS 0
-#endif
 // Priority schedule: a wave lowers its issue priority (s_setprio 3 -> 0) as
 // its item progresses, so that waves that are behind win the arbitration.
 // Hardware age order alone lets the oldest workgroup of a CU run ahead and
@@ -230,23 +223,6 @@ template <int P, int at, int T = 7> __device__ __forceinline__ void prio() {
     if constexpr (v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
 }
 
-__device__ __forceinline__ void stamp(const PassArgs& a, int i) {
-#if RS16_STAMPS
-    if (a.stamps && threadIdx.x == 0) {
-        a.stamps[blockIdx.x * 16 + i] = __builtin_amdgcn_s_memtime();
-        if (i == 0) {
-            a.stamps[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memrealtime();
-            // slots 12 / 13: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
-            a.stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            a.stamps[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-        }
-        if (i == 11) a.stamps[blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memrealtime();
-    }
-#else
-    (void)a;
-    (void)i;
-#endif
-}
 
 // s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
 // (expcnt and lgkmcnt at their maxima, i.e. not waited for).
@@ -1251,7 +1227,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         bool skip_a = false;
         if constexpr (ZERO_SKIP) skip_a = __all(d.zrow == (1u << NR) - 1);
         if (!skip_a) layers<P, T, false, 0, R, false, false>(L, H, c, a, tab1, tab2);
-        stamp(a, 3);
+        RS16_STAMP(a, 3);
         prio<P, 1, T>();
         if constexpr (T > 4) {
             Stager<T, (LateS2<P, T>::value ? G::TSPLIT : 0)> s3;
@@ -1271,12 +1247,12 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                         }
                     }
                 });
-            stamp(a, 4);
+            RS16_STAMP(a, 4);
             layers<P, T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
                                                                                                 tab2, d.zmask);
             in_b = true;
         }
-        stamp(a, 5);
+        RS16_STAMP(a, 5);
         prio<P, 2, T>();
     }
     // ---------------- formal derivative (tile bits) ----------------
@@ -1288,7 +1264,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
             if (in_b) tile_fd<T, NQR, true>(L, H, L, H, c, lds);
             else tile_fd<T, NQR, false>(L, H, L, H, c, lds);
         }
-        stamp(a, 6);
+        RS16_STAMP(a, 6);
     }
     // ---------------- FFT ----------------
     if constexpr (PT::FFT) {
@@ -1307,7 +1283,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                     }
                 }
             }
-            stamp(a, 7);
+            RS16_STAMP(a, 7);
             prio<P, 3, T>();
             // reveal multipliers: requested before the last layout switch,
             // written to LDS between its barriers (read after the layers)
@@ -1328,7 +1304,7 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                     if constexpr (LateReveal<P, T>::value) rs.commit(a, c, smem);
                 });
             }
-            stamp(a, 8);
+            RS16_STAMP(a, 8);
             prio<P, 4, T>();
             in_b = false;
         }
@@ -1343,14 +1319,11 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         } else if (need) {
             layers<P, T, false, 0, R, true, (TWO && !(SM::RESTAGE))>(L, H, c, a, tab1, tab2);
         }
-        stamp(a, 9);
+        RS16_STAMP(a, 9);
     }
     if constexpr (EARLY) {
-        stamp(a, 10);
-#if RS16_STAMPS
-        __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
-        stamp(a, 11);
-#endif
+        RS16_STAMP(a, 10);
+        RS16_STAMP_END(a);
         return;
     }
 
@@ -1371,11 +1344,8 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     asm volatile("" : "+v"(cs.offL));
     if (a.voff32) store_rows<P, T, true>(a, cs, L, H, rvt, lostf);
     else store_rows<P, T, false>(a, cs, L, H, rvt, lostf);
-    stamp(a, 10);
-#if RS16_STAMPS
-    __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
-    stamp(a, 11);
-#endif
+    RS16_STAMP(a, 10);
+    RS16_STAMP_END(a);
 }
 
 // The pass: workgroup b processes item b of the launch (4 waves per SIMD,
@@ -1439,7 +1409,7 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     // costs more VGPRs than the 128 of four waves per SIMD).  The twiddle
     // tables are requested first, the tile's rows right behind them, so the
     // staging latency hides under the row loads.
-    stamp(a, 0);
+    RS16_STAMP(a, 0);
     // Load-issue order: the workgroup in slot 0 of its CU (HW_ID.tg_id) issues
     // its rows first, slot 1 next, ...  Same-box A/B: kernel times equal,
     // step time -2 % (643-645 -> 654-659 GiB/s, 3 pairs).  The progress-based
@@ -1470,10 +1440,10 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
             a.need_hi = min(a.need_hi, any ? ((r1 - 1) >> a.lo) + 1 : 0u);
         }
     }
-    stamp(a, 1);
+    RS16_STAMP(a, 1);
     prio<P, 0, T>();
     st.template finish<EARLY>(a, c, smem);
-    stamp(a, 2);
+    RS16_STAMP(a, 2);
     process_item<P, T>(a, c, tile, slab, cur, smem);
 }
 
@@ -1703,9 +1673,9 @@ hipError_t launch_pass(int prog, int T, const PassArgs& args, uint32_t num_tiles
         const uint64_t span = (uint64_t)1 << (T + a.lo);  // rows of one tile's aligned block
         const bool fits = (hws - 1) * ((uint64_t)16 << a.lo) * smax + 1024 < ((uint64_t)1 << 32);
         const bool aligned = a.chunk % span == 0 && a.row_base_in % span == 0;
-        // (rs16_set_diagnostics RS16_DIAG_FORCE_VOFF64: always the 64-bit lane offsets)
-        a.voff32 = fits && aligned && !(g_diag & DIAG_FORCE_VOFF64) ? 1u : 0u;
-        a.fd_lds = (g_diag & DIAG_FD_LDS) ? 1u : 0u;
+        // (RS16_DIAG_FORCE_VOFF64: always the 64-bit lane offsets)
+        a.voff32 = fits && aligned && !(a.diag & DIAG_FORCE_VOFF64) ? 1u : 0u;
+        a.fd_lds = (a.diag & DIAG_FD_LDS) ? 1u : 0u;
     }
     const size_t lds = (size_t)kSmem[prog][T];
     if (lds > 65536) {

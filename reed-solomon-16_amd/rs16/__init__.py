@@ -30,19 +30,35 @@ __all__ = [
     "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS", "set_diagnostics",
     "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL", "DIAG_NO_COLUMN", "DIAG_FORCE_COLUMN",
     "DIAG_TILE_LAST", "DIAG_NO_TILE_LAST", "DIAG_FD_LDS", "DIAG_COL_RADIX4", "encode_host", "decode_host",
+    "encode_host_batch", "decode_host_batch",
     "encode_host_multi", "decode_host_multi", "Comm", "column_slice", "scatter_columns", "gather_columns",
 ]
 
 GF_ORDER = 65536
 GF_MODULUS = 65535
-# rs16_set_diagnostics flags (include/rs16.h): alternative code paths for tests
+# rs16_engine_set_diagnostics flags (include/rs16.h): alternative code paths for tests
 DIAG_FORCE_VOFF64, DIAG_EVAL_TWO_KERNEL, DIAG_EVAL_FULL, DIAG_NO_COLUMN, DIAG_FORCE_COLUMN = 1, 2, 4, 8, 16
 DIAG_TILE_LAST, DIAG_NO_TILE_LAST, DIAG_FD_LDS, DIAG_COL_RADIX4 = 32, 64, 128, 256
+# Test convenience only: the flags set_diagnostics() without an engine gave
+# every live engine, and that engines created later in this Python process
+# start with.  The library itself keeps the switches per engine.
+_diag_default = 0
 
 
-def set_diagnostics(flags: int) -> int:
-    """Process-wide diagnostic switches (identical results); returns the previous flags."""
-    return lib().rs16_set_diagnostics(flags)
+def set_diagnostics(flags: int, engine: Optional["Engine"] = None) -> int:
+    """Diagnostic switches (identical results); returns the previous flags.
+
+    With an engine: that engine's switches (rs16_engine_set_diagnostics).
+    Without: every live engine's, and those of engines created afterwards
+    in this process (a test helper; returns the previous default)."""
+    global _diag_default
+    if engine is not None:
+        return engine.set_diagnostics(flags)
+    old, _diag_default = _diag_default, flags
+    for e in list(_live_engines):
+        if getattr(e, "h", None):
+            e.set_diagnostics(flags)
+    return old
 RATE_DEFAULT, RATE_HIGH, RATE_LOW = 0, 1, 2
 _RATES = {"default": 0, "high": 1, "low": 2, 0: 0, 1: 1, 2: 2}
 
@@ -161,6 +177,12 @@ class Engine:
             raise Error._from_c(self._err)
         self.device = device
         _live_engines.add(self)
+        if _diag_default:
+            self.set_diagnostics(_diag_default)
+
+    def set_diagnostics(self, flags: int) -> int:
+        """This engine's diagnostic switches (include/rs16.h); returns the previous ones."""
+        return lib().rs16_engine_set_diagnostics(self.h, flags)
 
     def close(self):
         if getattr(self, "h", None):
@@ -697,6 +719,31 @@ def decode_host(original_count, recovery_count, shard_bytes, h_original, origina
     _check(lib().rs16_decode_host(eng.h, original_count, recovery_count, shard_bytes, _host_ptr(h_original),
                                   _host_ptr(original_received), _host_ptr(h_recovery),
                                   _host_ptr(recovery_received), slice_bytes, C.byref(err)), err)
+
+
+def encode_host_batch(original_count, recovery_count, shard_bytes, nstripes, h_original, original_stride,
+                      h_recovery, recovery_stride, engine: Optional[Engine] = None):
+    """nstripes host-resident stripes, two in flight (rs16_encode_host_batch):
+    stripe i + 1's host->device copy and stripe i - 1's device->host copy
+    overlap stripe i's codec."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_encode_host_batch(eng.h, original_count, recovery_count, shard_bytes, nstripes,
+                                        _host_ptr(h_original), original_stride, _host_ptr(h_recovery),
+                                        recovery_stride, C.byref(err)), err)
+
+
+def decode_host_batch(original_count, recovery_count, shard_bytes, nstripes, h_original, original_stride,
+                      original_received, original_received_stride, h_recovery, recovery_stride, recovery_received,
+                      recovery_received_stride, engine: Optional[Engine] = None):
+    """rs16_decode_host_batch: every stripe with its own host flag bytes; lost
+    originals restored in place into h_original."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_decode_host_batch(eng.h, original_count, recovery_count, shard_bytes, nstripes,
+                                        _host_ptr(h_original), original_stride, _host_ptr(original_received),
+                                        original_received_stride, _host_ptr(h_recovery), recovery_stride,
+                                        _host_ptr(recovery_received), recovery_received_stride, C.byref(err)), err)
 
 
 def _engine_array(engines):

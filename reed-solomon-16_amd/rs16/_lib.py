@@ -30,7 +30,7 @@ SIGNATURES = {
     "rs16_engine_profile_read": (_i, [_p, _i, C.POINTER(C.c_double), C.POINTER(C.c_uint64), _e]),
     "rs16_engine_profile_reset": (None, [_p]),
     "rs16_prog_count": (_i, []),
-    "rs16_set_diagnostics": (_i, [_i]),
+    "rs16_engine_set_diagnostics": (_i, [_p, _i]),
     "rs16_prog_name": (C.c_char_p, [_i]),
     "rs16_engine_set_stamps": (_i, [_p, _p, _i, _e]),
     "rs16_engine_set_slices": (_i, [_p, _i, _e]),
@@ -105,6 +105,8 @@ SIGNATURES = {
     "rs16_scatter_columns_virtual": (_i, [_p, _i, _sz, _sz, _p, _p, _p, _e]),
     "rs16_gather_columns_virtual": (_i, [_p, _i, _sz, _sz, _p, _p, _p, _e]),
     "rs16_encode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _e]),
+    "rs16_encode_host_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _sz, _e]),
+    "rs16_decode_host_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _sz, _p, _sz, _p, _sz, _e]),
     "rs16_decode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _p, _p, _e]),
     "rs16_stream_create": (_p, [_p, _e]),
     "rs16_stream_destroy": (None, [_p, _p]),

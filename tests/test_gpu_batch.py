@@ -162,6 +162,8 @@ def _varied_masks(k, m, n, seed, mode):
     (32768, 32768, 64, 2, "mixed"),     # the 65536-row decode, T = 8 passes finishing eval's last H_lo
     (300, 3000, 64, 3, "mixed"),        # low rate
     (3, 5, 64, 7, "mixed"),
+    (100, 100, 64, 300, "mixed"),       # more stripes than one group (256): two groups of eval + passes
+    (3, 5, 64, 513, "mixed"),           # three groups, the last of one stripe
 ])
 def test_decode_batch_varied(k, m, sb, n, mode):
     # stripes with losses of their own, one call; every

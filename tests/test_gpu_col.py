@@ -158,6 +158,30 @@ def test_col_rate_api_in_place(eng, rate, k, m):
     assert all(np.array_equal(np.frombuffer(got[i], np.uint8), original[i]) for i in range(lost))
 
 
+@pytest.mark.parametrize("k,m", [
+    # low rate, 128-row chunks (colm_kernel: one wave per recovery chunk)
+    (100, 1000), (65, 300), (128, 2048),
+    # low rate, 256-1024-row chunks (a workgroup per quad column and recovery chunk)
+    (300, 2000), (200, 1500), (1000, 3000), (1000, 6000), (512, 2100),
+    # high rate multi-chunk (chunk IFFTs, then the FFT of their XOR)
+    (1000, 100), (3000, 1000), (2000, 300)])
+@pytest.mark.parametrize("sb", [64, 1024])
+def test_col_multi_chunk_rate_api_in_place(eng, k, m, sb):
+    """Multi-chunk encodes through the Rate API, whose work buffer holds the
+    originals and receives the recovery in place (rate_low.rs:44-83,
+    rate_high.rs:44-83): no workgroup may overwrite originals another one
+    has not read yet (chunk 0's recovery rows overlay them)."""
+    original = generate_original(k, sb, 13 * k + m + sb)
+    want = O.encode(k, m, original)
+    for rnd in range(2):  # (a second round on the same encoder: stale rows in the buffer)
+        enc = rs16.ReedSolomonEncoder(k, m, sb, engine=eng)
+        for o in original:
+            enc.add_original_shard(o)
+        with enc.encode() as res:
+            rec = np.stack([np.frombuffer(r, np.uint8) for r in res.recovery_iter()])
+        assert np.array_equal(rec, want), rnd
+
+
 @pytest.mark.parametrize("k,m,n,sb", [(1000, 1000, 5, 128), (512, 512, 3, 128), (300, 1000, 4, 128),
                                       (1000, 1000, 6, 1024), (100, 100, 7, 192)])
 def test_col_batched_stripes(eng, k, m, n, sb, force_column, form):

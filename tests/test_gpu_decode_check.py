@@ -70,3 +70,37 @@ def test_counts_checked_nothing_to_restore(k, m):
         rs16.decode_device(k, m, sb, d_o.ptr, d_fo.ptr, d_r.ptr, d_fr.ptr, k, 3, engine=eng, check=True)
     assert e.value.kind == "InvalidArgument"
     assert np.array_equal(d_o.download(shape=(k, sb)), orig)  # nothing written
+
+
+def test_nothing_to_restore_snapshot_and_null_flags():
+    # the check of a decode with nothing to restore counts a copy
+    # of the flags taken at the decode's place in stream order, so flag arrays
+    # the caller rewrites (or frees) afterwards do not change the answer, and
+    # a NULL flag array counts as "none received".
+    import ctypes as C
+    from rs16._lib import RS16Error, lib
+
+    eng = rs16.Engine(0)
+    k, m, sb = 300, 300, 64
+    orig = generate_original(k, sb, 6)
+    d_o, d_r = DeviceArray.from_numpy(eng, orig), DeviceArray(eng, m * sb)
+    rs16.encode_device(k, m, sb, d_o.ptr, d_r.ptr, engine=eng)
+    om = np.ones(k, np.uint8)
+    rm = np.zeros(m, np.uint8)
+    rm[:5] = 1
+    d_fo, d_fr = DeviceArray.from_numpy(eng, om), DeviceArray.from_numpy(eng, rm)
+    rs16.decode_device(k, m, sb, d_o.ptr, d_fo.ptr, d_r.ptr, d_fr.ptr, k, 5, engine=eng)
+    # the caller reuses its flag arrays before checking: the check still sees
+    # the flags the decode was given
+    d_fo.upload(np.zeros(k, np.uint8))
+    d_fr.upload(np.ones(m, np.uint8))
+    err = RS16Error()
+    assert lib().rs16_decode_check(eng.h, None, C.byref(err)) == 0, err.code
+    # NULL recovery flags with a zero recovery count: OK; with a nonzero count: detected
+    d_fo.upload(om)
+    rs16.decode_device(k, m, sb, d_o.ptr, d_fo.ptr, d_r.ptr, 0, k, 0, engine=eng, check=True)
+    with pytest.raises(rs16.Error) as e:
+        rs16.decode_device(k, m, sb, d_o.ptr, d_fo.ptr, d_r.ptr, 0, k, 2, engine=eng, check=True)
+    assert e.value.kind == "InvalidArgument"
+    assert np.array_equal(d_o.download(shape=(k, sb)), orig)
+    eng.close()

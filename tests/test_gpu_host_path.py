@@ -85,3 +85,79 @@ def test_host_slots_own_scratch(eng, k, m, sb, slice_bytes, loss):
         horig[k - L:] = 0x5A
         rs16.decode_host(k, m, sb, horig, of, hrec, rf, slice_bytes, engine=eng)
         assert np.array_equal(horig, original), f"decode, repetition {rep}"
+
+
+@pytest.mark.parametrize("k,m,sb,n,pinned,pattern", [
+    (1000, 1000, 1024, 5, True, "all"),       # column codec, half decode, odd stripe count
+    (1000, 1000, 1024, 4, False, "mixed"),    # pageable buffers
+    (4096, 4096, 256, 6, True, "mixed"),      # pass codec, per-stripe losses (some stripes lose nothing)
+    (3000, 30000, 128, 3, True, "mixed"),     # low rate
+    (100, 3, 64 * 5, 7, True, "scatter"),     # multi-chunk high rate
+    (32768, 32768, 64, 3, True, "all"),       # max shard count
+    (50, 60, 64, 1, True, "scatter"),         # one stripe
+])
+def test_host_batch_pipelined(eng, k, m, sb, n, pinned, pattern):
+    """rs16_encode_host_batch / rs16_decode_host_batch:
+    stripes with gaps between them, two in flight on two copy streams; every
+    stripe's recovery equals the oracle's, every lost original comes back,
+    received originals and the gaps are untouched."""
+    pad = 64
+    so, sr = k * sb + pad, m * sb + pad
+    stripes = [generate_original(k, sb, 40 + i) for i in range(n)]
+
+    def buf(nbytes, fill):
+        if pinned:
+            p = PinnedArray(eng, nbytes)
+            p.array[:] = fill
+            return p, p.array
+        return None, np.full(nbytes, fill, np.uint8)
+
+    keep_o, ho = buf(n * so, 0xEE)
+    keep_r, hr = buf(n * sr, 0x77)
+    for i, o in enumerate(stripes):
+        ho[i * so:i * so + k * sb] = o.reshape(-1)
+    rs16.encode_host_batch(k, m, sb, n, ho, so, hr, sr, engine=eng)
+    recs = []
+    for i, o in enumerate(stripes):
+        rec = hr[i * sr:i * sr + m * sb].reshape(m, sb)
+        assert np.array_equal(rec, O.encode(k, m, o)), i
+        assert (hr[i * sr + m * sb:(i + 1) * sr] == 0x77).all(), i
+        recs.append(rec.copy())
+    # per-stripe loss patterns
+    rng = np.random.default_rng(k + n)
+    fso, fsr = k + 1, m + 3
+    fo = np.zeros(n * fso, np.uint8)
+    fr = np.zeros(n * fsr, np.uint8)
+    for i in range(n):
+        kind = pattern if pattern != "mixed" else ("all", "scatter", "none")[i % 3]
+        om, rm = np.ones(k, bool), np.zeros(m, bool)
+        lost = min(k, m)
+        if kind == "all":
+            om[:lost] = False
+        elif kind == "scatter":
+            om[rng.choice(k, int(rng.integers(1, lost + 1)), replace=False)] = False
+        rm[rng.choice(m, min(m, int((~om).sum()) + 1), replace=False)] = True
+        fo[i * fso:i * fso + k] = om
+        fr[i * fsr:i * fsr + m] = rm
+        seg = ho[i * so:i * so + k * sb].reshape(k, sb)
+        seg[~om] = 0xA5
+        hr[i * sr:i * sr + m * sb].reshape(m, sb)[~rm] = 0x3C  # not-received recovery holds garbage
+    rs16.decode_host_batch(k, m, sb, n, ho, so, fo, fso, hr, sr, fr, fsr, engine=eng)
+    for i, o in enumerate(stripes):
+        assert np.array_equal(ho[i * so:i * so + k * sb].reshape(k, sb), o), i
+        assert (ho[i * so + k * sb:(i + 1) * so] == 0xEE).all(), i
+
+
+def test_host_batch_errors(eng):
+    k, m, sb = 10, 5, 64
+    ho, hr = np.zeros(3 * k * sb, np.uint8), np.zeros(3 * m * sb, np.uint8)
+    fo, fr = np.ones(3 * k, np.uint8), np.zeros(3 * m, np.uint8)
+    fo[k:k + 7] = 0  # stripe 1 lost 7 originals with no recovery shard
+    with pytest.raises(rs16.Error) as e:
+        rs16.decode_host_batch(k, m, sb, 3, ho, k * sb, fo, k, hr, m * sb, fr, m, engine=eng)
+    assert e.value == rs16.Error("NotEnoughShards", original_count=k, original_received_count=3,
+                                 recovery_received_count=0)
+    with pytest.raises(rs16.Error) as e:  # stride below a stripe
+        rs16.encode_host_batch(k, m, sb, 2, ho, k * sb - 64, hr, m * sb, engine=eng)
+    assert e.value.kind == "InvalidArgument"
+    rs16.encode_host_batch(k, m, sb, 0, ho, k * sb, hr, m * sb, engine=eng)  # no stripes: OK
