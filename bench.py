@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--recovery", type=int, default=32768)
     p.add_argument("--shard-bytes", type=int, default=1024)
     p.add_argument("--slices", type=int, default=1, help="concurrent column slices of the device codec")
+    p.add_argument("--split-decode", action="store_true",
+                   help="issue the step's decode split (rs16_decode_prepare on a side stream during the encode)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1000:1000 side measurements")
@@ -398,63 +400,89 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
     per engine / stream, so that one stripe's load and store phases overlap
     the other's butterflies; and the producer / consumer form, engine A
     encoding a stripe while engine B decodes another one's (already encoded)
-    recovery.  Both restorations are checked."""
+    recovery.  Both restorations are checked.
+
+    Some stream pairs share a hardware queue and then run one stripe after
+    the other (scripts/probe_queues.py): the second engine is
+    taken from up to 4 candidates, the first whose pair overlaps (two stripes
+    in < 1.6 x the time of one); the first candidate's rate is reported too."""
     import numpy as np
 
     import rs16
     from rs16.device import DeviceArray
     from rs16.util import generate_original
 
-    eng2 = rs16.Engine(local)
     o2 = generate_original(k, S, 1)
-    a2, r2, x2 = DeviceArray.from_numpy(eng2, o2), DeviceArray(eng2, m * S), DeviceArray(eng2, k * S)
-    f2o, f2r = DeviceArray.from_numpy(eng2, of), DeviceArray.from_numpy(eng2, rf)
-    if loss < k:
-        x2.upload(o2)
+    step_bytes = 2 * (k + m) * S
 
-    def enc2():
-        rs16.encode_device(k, m, S, a2.ptr, r2.ptr, engine=eng2)
+    def run(engs, body, steps, warmup):
+        for _ in range(warmup):
+            body()
+        for e in engs:
+            e.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            body()
+        for e in engs:
+            e.synchronize()
+        return time.perf_counter() - t0
 
-    def dec2():
-        rs16.decode_device(k, m, S, x2.ptr, f2o.ptr, r2.ptr, f2r.ptr, k - loss, loss, engine=eng2)
-
-    def two():
+    def one():
         encode()
-        enc2()
         decode()
-        dec2()
+
+    t1 = run([eng], one, 10, 3) / 10
+    tried = []
+    chosen = None
+    for cand in range(4):
+        eng2 = rs16.Engine(local)
+        a2, r2, x2 = DeviceArray.from_numpy(eng2, o2), DeviceArray(eng2, m * S), DeviceArray(eng2, k * S)
+        f2o, f2r = DeviceArray.from_numpy(eng2, of), DeviceArray.from_numpy(eng2, rf)
+        if loss < k:
+            x2.upload(o2)
+
+        def enc2():
+            rs16.encode_device(k, m, S, a2.ptr, r2.ptr, engine=eng2)
+
+        def dec2():
+            rs16.decode_device(k, m, S, x2.ptr, f2o.ptr, r2.ptr, f2r.ptr, k - loss, loss, engine=eng2)
+
+        def two():
+            encode()
+            enc2()
+            decode()
+            dec2()
+
+        two()
+        eng2.synchronize()
+        assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
+        ratio = run([eng, eng2], two, 10, 3) / 10 / t1
+        tried.append(round(ratio, 3))
+        if ratio < 1.6 or cand == 3:
+            chosen = (eng2, a2, r2, x2, f2o, f2r, enc2, dec2, two)
+            break
+        del a2, r2, x2, f2o, f2r
+        eng2.close()
+    eng2, a2, r2, x2, f2o, f2r, enc2, dec2, two = chosen
 
     def enc_dec():
         encode()
         dec2()
 
-    def run(body, steps):
-        for _ in range(args.warmup):
-            body()
-        eng.synchronize()
-        eng2.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            body()
-        eng.synchronize()
-        eng2.synchronize()
-        return time.perf_counter() - t0
-
-    two()
-    eng2.synchronize()
-    assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
-    step_bytes = 2 * (k + m) * S
-    t2 = run(two, args.steps)
-    t3 = run(enc_dec, args.steps)
+    t2 = run([eng, eng2], two, args.steps, args.warmup)
+    t3 = run([eng, eng2], enc_dec, args.steps, args.warmup)
     assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
     del a2, r2, x2, f2o, f2r
     eng2.close()
     return {"gib_s": 2 * step_bytes * args.steps / t2 / GIB, "ms_per_two_stripes": t2 / args.steps * 1e3,
             "encode_while_decode_gib_s": step_bytes * args.steps / t3 / GIB,
             "encode_while_decode_us": t3 / args.steps * 1e6, "where": where,
+            "second_engine_candidates": tried,
+            "first_candidate_gib_s": 2 * step_bytes / (tried[0] * t1) / GIB,
             "note": "serving-mode throughput: two independent 32768:32768 x 1 KiB stripes in flight "
                     "(gib_s), or one stripe encoding on engine A while another's recovery decodes on "
-                    "engine B (encode_while_decode); not the metric"}
+                    "engine B (encode_while_decode); candidates = two-stripe time / one-stripe time per "
+                    "second engine tried (a pair on one hardware queue runs serially, ~2.0); not the metric"}
 
 
 def main():
@@ -551,9 +579,29 @@ def main():
             dt = float(t.item())
         return dt
 
-    def step():
+    # The step: encode the stripe, then decode its recovery at 100 % original
+    # loss (encode, then rs16_decode_device, on the engine stream).  With
+    # --split-decode the decode's erasure locator (rs16_decode_prepare, DESIGN.md
+    # 3.12) is computed on a side stream while the encode runs; measured slower
+    # (the locator's workgroups take slots from the encode's first pass, and the
+    # cross-stream wait costs more than the 9 us it hides), so it is an extra.
+    side = eng.create_stream()
+
+    def step_serial():
         encode()
         decode()
+
+    def step_split():
+        rs16.decode_prepare(k, m, S, d_of.ptr, d_rf.ptr, k - loss, loss, stream=side, engine=eng)
+        encode()
+        rs16.decode_device_prepared(k, m, S, d_rest.ptr, d_rec.ptr, engine=eng)
+
+    step = step_split if args.split_decode else step_serial
+    held = original.copy()
+    held[:loss] = 0
+    d_rest.upload(held)
+    step_split()
+    assert args.no_verify or np.array_equal(d_rest.download(shape=(k, S)), original), "split decode did not restore"
 
     # ---- roofline: dominant kernel, hipEvent-timed on its launch stream ----
     # An event-profiled copy of the K-step loop, run BEFORE the W warm-up
@@ -583,9 +631,17 @@ def main():
     value = world * step_bytes * args.steps / dt / GIB
     ms_per_step = dt / args.steps * 1e3
 
-    # Separate encode-only / decode-only rates (same data, same engine).
+    # Separate encode-only / decode-only rates (same data, same engine), and
+    # the step issued the other way (split / serial decode).
     dt_e = timed(encode, args.steps)
     dt_d = timed(decode, args.steps)
+    other = step_serial if args.split_decode else step_split
+    for _ in range(args.warmup):
+        other()
+    dt_o = timed(other, args.steps)
+    other_step = {"gib_s": world * step_bytes * args.steps / dt_o / GIB, "ms_per_step": dt_o / args.steps * 1e3,
+                  "decode_issue": "serial: rs16_decode_device" if args.split_decode else
+                  "split: rs16_decode_prepare on a side stream during the encode, then rs16_decode_device_prepared"}
     two_early = None
     if not args.no_extra and world == 1:
         # the serving-mode rate measured right here as well as after the
@@ -637,7 +693,7 @@ def main():
                         "wave-quad-butterfly, profiles/r03_ubench_bfly.txt) at 2.4 GHz; the zero-twiddle groups "
                         "the two-direction passes skip still count as butterflies here"}
 
-    extra = {}
+    extra = {"serial_step" if args.split_decode else "split_decode_step": other_step}
     if not args.no_extra:
         extra["sustained"] = sustained(eng, step, step_bytes * world, dist)
     if not args.no_extra and (k, m) != (1000, 1000):
@@ -816,10 +872,8 @@ def main():
     if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
         extra["configs4_rccl"] = configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, args.steps)
 
-    if not args.no_extra and world == 1:
-        extra["two_stripes_two_streams"] = two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args,
-                                                       "after the other extras (the r04 position)")
-        extra["two_stripes_two_streams"]["right_after_timed_loop"] = two_early
+    if two_early is not None:
+        extra["two_stripes_two_streams"] = two_early
 
     if not args.no_extra:
         # Shards that start and end in host memory (north_star: recorded beside
@@ -918,7 +972,10 @@ def main():
                         " (BASELINE configs[1] + [2])" if (k, m, S) == (1000, 1000, 1024) else ""),
                        "original_count": k, "recovery_count": m, "shard_bytes": S,
                        "parallelism": f"independent stripes x {world} (weak, no collective)",
-                       "column_slices": args.slices},
+                       "column_slices": args.slices,
+                       "decode_issue": ("split: rs16_decode_prepare (eval_poly of the received pattern) on a side "
+                                        "stream while the encode runs, then rs16_decode_device_prepared"
+                                        if args.split_decode else "serial: rs16_decode_device after the encode")},
             "encode_gib_s": round(world * (k + m) * S * args.steps / dt_e / GIB, 3),
             "decode_gib_s": round(world * (k + m) * S * args.steps / dt_d / GIB, 3),
             "roofline": roofline,

@@ -308,6 +308,33 @@ int rs16_decode_host(rs16_engine* eng, size_t original_count, size_t recovery_co
                      void* h_original, const uint8_t* original_received, const void* h_recovery,
                      const uint8_t* recovery_received, size_t slice_bytes, rs16_error* err);
 
+/* ---- Split device decode -------------------------------------------------
+ * rs16_decode_device in two halves on two streams.  rs16_decode_prepare
+ * takes the received pattern only (the same flags / counts and checks as
+ * rs16_decode_device: UnsupportedShardCount, InvalidArgument,
+ * NotEnoughShards) and enqueues the erasure locator, eval_poly of the
+ * erasure vector (src/rate/rate_high.rs:168-202, src/engine.rs:207-218), on
+ * `stream`; rs16_decode_device_prepared then runs the rest of the decode
+ * (src/rate/rate_high.rs:203-247) on its own stream, ordered after the
+ * preparation.  The pattern of a decode is known before its shards are (a
+ * storage system knows which devices failed), so the locator can be computed
+ * while the shards are still being produced or copied in: work the caller
+ * issues on the engine between the two calls that does not decode -- e.g.
+ * the encode of the stripe whose recovery is about to be decoded -- runs
+ * concurrently with the preparation.  One preparation per engine, consumed
+ * by the next rs16_decode_device_prepared with the same (k, m, shard_bytes)
+ * (else InvalidArgument); any other decode on the engine in between orders
+ * itself after the preparation and discards it.  The flag arrays must keep
+ * their contents until the prepared decode has run.  Results are those of
+ * rs16_decode_device; rs16_decode_check covers the prepared decode. */
+int rs16_decode_prepare(rs16_engine* eng, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                        const uint8_t* d_original_received, const uint8_t* d_recovery_received,
+                        size_t original_received_count, size_t recovery_received_count, void* stream,
+                        rs16_error* err);
+int rs16_decode_device_prepared(rs16_engine* eng, size_t original_count, size_t recovery_count,
+                                size_t shard_bytes, void* d_original, const void* d_recovery, void* stream,
+                                rs16_error* err);
+
 /* ---- Host-resident stripes, pipelined (full duplex) -----------------------
  * nstripes independent stripes in host memory (stripe i's originals at
  * h_original + i original_stride, its recovery at h_recovery + i

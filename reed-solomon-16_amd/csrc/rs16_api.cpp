@@ -132,7 +132,7 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
     } else {
         const size_t chunks = ((size_t)g.n + 63) / 64;
         std::vector<uint32_t> c(2 * chunks);
-        RS16_HIP(hipMemcpy(c.data(), e->ws_rcount.p, c.size() * 4, hipMemcpyDeviceToHost));
+        RS16_HIP(hipMemcpy(c.data(), e->ev_main.rcount.p, c.size() * 4, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < chunks; i++) a += c[2 * i], b += c[2 * i + 1];
     }
     // (orig_recv, rec_recv) as the caller gave them to rs16_decode_device
@@ -267,23 +267,20 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->ws_z.release();
     e->ws_u.release();
     e->ws_fd.release();
-    e->ws_work32.release();
-    e->ws_elog.release();
+    e->ev_main.release();
+    for (auto& l : e->ev_lane) l.release();
     e->ws_flags.release();
     e->hp_flags.release();
-    e->ws_zflag.release();
-    e->ws_rbits.release();
-    e->ws_lost.release();
-    e->ws_rcount.release();
     for (auto& sl : e->hslot) {
         if (sl.s) (void)hipStreamSynchronize(sl.s), (void)hipStreamDestroy(sl.s);
         sl.orig.release(), sl.rec.release(), sl.z.release(), sl.u.release();
     }
     e->hflags.release();
     if (e->hev) (void)hipEventDestroy(e->hev);
-    for (auto& row : e->hp_ev)
-        for (auto& ev : row)
-            if (ev) (void)hipEventDestroy(ev);
+    if (e->prep_ev) (void)hipEventDestroy(e->prep_ev);
+    for (auto& ev : e->hp_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->hp_off) (void)hipEventDestroy(e->hp_off);
     if (e->order_ev) (void)hipEventDestroy(e->order_ev);
     for (int j = 0; j < rs16_engine::MAX_SLICES; j++) {
         if (e->sl_own[j]) (void)hipStreamDestroy(e->sl_own[j]);
@@ -346,8 +343,9 @@ extern "C" int rs16_engine_fwht(rs16_engine* e, uint16_t* d, size_t trunc, void*
     if (trunc > GF_ORDER) return set_error(err, RS16_INVALID_ARGUMENT);
     if (int rc = e->activate(err)) return rc;
     if (int rc = e->order(e->pick(stream), err)) return rc;
-    RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
-    RS16_HIP(launch_fwht_u16(d, (uint32_t*)e->ws_work32.p, e->pick(stream)));
+    if (int rc = e->guard_eval(e->pick(stream), false, err)) return rc;
+    RS16_HIP(e->evset->work32.reserve(GF_ORDER * 4));
+    RS16_HIP(launch_fwht_u16(d, (uint32_t*)e->evset->work32.p, e->pick(stream)));
     if (int rc = e->scratch_done(e->pick(stream), err)) return rc;
     return set_error(err, RS16_OK);
 }
@@ -355,8 +353,9 @@ extern "C" int rs16_engine_eval_poly(rs16_engine* e, uint16_t* d, size_t trunc, 
     if (trunc > GF_ORDER) return set_error(err, RS16_INVALID_ARGUMENT);
     if (int rc = e->activate(err)) return rc;
     if (int rc = e->order(e->pick(stream), err)) return rc;
-    RS16_HIP(e->ws_work32.reserve(GF_ORDER * 4));
-    RS16_HIP(launch_eval_poly_u16(d, (uint32_t*)e->ws_work32.p, e->d_log_walsh, e->pick(stream)));
+    if (int rc = e->guard_eval(e->pick(stream), false, err)) return rc;
+    RS16_HIP(e->evset->work32.reserve(GF_ORDER * 4));
+    RS16_HIP(launch_eval_poly_u16(d, (uint32_t*)e->evset->work32.p, e->d_log_walsh, e->pick(stream)));
     if (int rc = e->scratch_done(e->pick(stream), err)) return rc;
     return set_error(err, RS16_OK);
 }
@@ -1077,44 +1076,27 @@ extern "C" int rs16_decode_host(rs16_engine* e, size_t k, size_t m, size_t S, vo
 }
 
 // ---------------------------------------------------------------------------
-// Host-resident stripes, pipelined.  Three streams: hslot[0].s copies inputs
-// in, the engine stream runs the codec, hslot[1].s copies outputs back.
-// Device buffers alternate by stripe parity b (hslot[b].orig / .rec; the
-// codec's scratch ws_z / ws_u is used only on the engine stream).  Stripe i:
-//   H2D  : [i >= 2: wait codec(i - 2) done with buffers b; decode: and its
-//          D2H, which reads the originals restored in place] copy in, record h2d[b]
-//   codec: wait h2d[b] [, i >= 2: wait d2h(i - 2) done reading buffers b]
-//          encode / decode, record codec[b]
-//   D2H  : wait codec[b], copy out, record d2h[b]
-// (a hipStreamWaitEvent waits for the event's latest record at the time of
-// the wait, which the enqueue order above makes the right stripe's).
+// Host-resident stripes, pipelined.  Two lanes, each a stream with device
+// buffers and codec scratch of its own (hslot[b]: rows, Z, U; ev_lane[b]:
+// the decode's eval_poly outputs): stripe i runs on lane i & 1 as
+// H2D -> codec -> D2H in stream order, so while one lane copies a stripe's
+// outputs back the other copies the next stripe's inputs in -- both link
+// directions busy -- and no event crosses between streams (the copy engines'
+// waits on other queues' events stalled the pipeline for milliseconds at a
+// time, profiles/r05_hostbatch_trace.txt).
 // ---------------------------------------------------------------------------
-int rs16_engine::host_pipe_events(rs16_error* err) {
-    for (auto& row : hp_ev)
-        for (auto& ev : row)
-            if (!ev) RS16_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    return RS16_OK;
-}
-
 namespace {
-enum { HP_H2D = 0, HP_CODEC = 1, HP_D2H = 2 };
 // Contiguous runs of rows whose flag equals `want` (rows [0, n)), each one
 // copy; more than max_runs of them: one copy of the span from the first to
 // the last such row.
 template <class F>
 int copy_runs(const uint8_t* flags, size_t n, bool want, size_t max_runs, F copy) {
     size_t runs = 0, first = n, last = 0;
-    for (size_t i = 0; i < n;) {
-        if ((flags[i] != 0) != want) {
-            i++;
-            continue;
-        }
-        size_t j = i;
-        while (j < n && (flags[j] != 0) == want) j++;
-        runs++;
+    for (size_t i = 0; i < n; i++) {
+        if ((flags[i] != 0) != want) continue;
+        if (i == 0 || (flags[i - 1] != 0) != want) runs++;
         first = std::min(first, i);
-        last = j;
-        i = j;
+        last = i + 1;
     }
     if (runs == 0) return RS16_OK;
     if (runs > max_runs) return copy(first, last - first);
@@ -1131,7 +1113,20 @@ int copy_runs(const uint8_t* flags, size_t n, bool want, size_t max_runs, F copy
     return RS16_OK;
 }
 constexpr size_t HP_MAX_RUNS = 64;
+// the engine's decode scratch set, restored on every exit path
+struct EvalSet {
+    rs16_engine* e;
+    explicit EvalSet(rs16_engine* eng, int lane) : e(eng) { e->evset = &e->ev_lane[lane]; }
+    ~EvalSet() { e->evset = &e->ev_main; }
+};
 }  // namespace
+
+int rs16_engine::host_pipe_events(rs16_error* err) {
+    for (auto& ev : hp_ev)
+        if (!ev) RS16_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (!hp_off) RS16_HIP(hipEventCreateWithFlags(&hp_off, hipEventDisableTiming));
+    return RS16_OK;
+}
 
 extern "C" int rs16_encode_host_batch(rs16_engine* e, size_t k, size_t m, size_t S, size_t nstripes,
                                       const void* h_original, size_t original_stride, void* h_recovery,
@@ -1146,35 +1141,28 @@ extern "C" int rs16_encode_host_batch(rs16_engine* e, size_t k, size_t m, size_t
     for (auto& sl : e->hslot) {
         RS16_HIP(sl.orig.reserve(k * S));
         RS16_HIP(sl.rec.reserve(m * S));
+        RS16_HIP(sl.z.reserve(wc * S));
+        if (!high) RS16_HIP(sl.u.reserve(next_pow2(k) * S));
     }
-    RS16_HIP(e->ws_z.reserve(wc * S));
-    int urc;
-    uint8_t* U = engine_u(e, high, k, S, err, &urc);
-    if (urc) return urc;
     if (int rc = e->host_pipe_events(err)) return rc;
-    if (int rc = e->host_slots(err)) return rc;  // (copy streams after the engine stream's earlier work)
-    hipStream_t cin = e->hslot[0].s, cout = e->hslot[1].s, cs = e->stream;
-    auto& ev = e->hp_ev;
+    if (int rc = e->host_slots(err)) return rc;  // (lanes after the engine stream's earlier work)
     for (size_t i = 0; i < nstripes; i++) {
-        const int b = (int)(i & 1);
-        uint8_t* d_o = (uint8_t*)e->hslot[b].orig.p;
-        uint8_t* d_r = (uint8_t*)e->hslot[b].rec.p;
-        if (i >= 2) RS16_HIP(hipStreamWaitEvent(cin, ev[HP_CODEC][b], 0));
+        auto& sl = e->hslot[i & 1];
+        uint8_t* d_o = (uint8_t*)sl.orig.p;
+        uint8_t* d_r = (uint8_t*)sl.rec.p;
+        // lane 1 starts half a period late (its first H2D after lane 0's), so
+        // that from then on one lane's D2H meets the other's H2D, not its D2H
+        if (i == 1) RS16_HIP(hipStreamWaitEvent(sl.s, e->hp_off, 0));
         RS16_HIP(hipMemcpyAsync(d_o, (const uint8_t*)h_original + i * original_stride, k * S, hipMemcpyHostToDevice,
-                                cin));
-        RS16_HIP(hipEventRecord(ev[HP_H2D][b], cin));
-        RS16_HIP(hipStreamWaitEvent(cs, ev[HP_H2D][b], 0));
-        if (i >= 2) RS16_HIP(hipStreamWaitEvent(cs, ev[HP_D2H][b], 0));
-        if (int rc = encode_dev(e, high, k, m, S, d_o, d_r, (uint8_t*)e->ws_z.p, U, cs, err)) return rc;
-        RS16_HIP(hipEventRecord(ev[HP_CODEC][b], cs));
-        RS16_HIP(hipStreamWaitEvent(cout, ev[HP_CODEC][b], 0));
-        RS16_HIP(hipMemcpyAsync((uint8_t*)h_recovery + i * recovery_stride, d_r, m * S, hipMemcpyDeviceToHost, cout));
-        RS16_HIP(hipEventRecord(ev[HP_D2H][b], cout));
+                                sl.s));
+        if (i == 0) RS16_HIP(hipEventRecord(e->hp_off, sl.s));
+        if (int rc = encode_dev(e, high, k, m, S, d_o, d_r, (uint8_t*)sl.z.p, high ? nullptr : (uint8_t*)sl.u.p, sl.s,
+                                err))
+            return rc;
+        RS16_HIP(hipMemcpyAsync((uint8_t*)h_recovery + i * recovery_stride, d_r, m * S, hipMemcpyDeviceToHost, sl.s));
     }
-    RS16_HIP(hipStreamSynchronize(cout));
-    RS16_HIP(hipStreamSynchronize(cin));
-    RS16_HIP(hipStreamSynchronize(cs));
-    if (int rc = e->scratch_done(cs, err)) return rc;
+    for (auto& sl : e->hslot) RS16_HIP(hipStreamSynchronize(sl.s));
+    if (int rc = e->scratch_done(e->stream, err)) return rc;
     return set_error(err, RS16_OK);
 }
 
@@ -1207,83 +1195,78 @@ extern "C" int rs16_decode_host_batch(rs16_engine* e, size_t k, size_t m, size_t
     for (auto& sl : e->hslot) {
         RS16_HIP(sl.orig.reserve(k * S));
         RS16_HIP(sl.rec.reserve(m * S));
+        RS16_HIP(sl.z.reserve((size_t)g0.n * S));
+        RS16_HIP(sl.u.reserve((size_t)g0.n * S));
+        RS16_HIP(sl.rcount.reserve(GF_ORDER / 64 * 8));
     }
-    RS16_HIP(e->ws_z.reserve((size_t)g0.n * S));
-    RS16_HIP(e->ws_u.reserve((size_t)g0.n * S));
     RS16_HIP(e->hflags.reserve(2 * (k + m)));
     RS16_HIP(e->hp_flags.reserve(2 * (k + m)));
     if (int rc = e->host_pipe_events(err)) return rc;
     if (int rc = e->host_slots(err)) return rc;
-    hipStream_t cin = e->hslot[0].s, cout = e->hslot[1].s, cs = e->stream;
     auto& ev = e->hp_ev;
+    int first_lane = -1;  // (lane offset: see rs16_encode_host_batch)
+    bool offset_pending = true;
     for (size_t i = 0; i < nstripes; i++) {
+        if (ocnt[i] == k) continue;  // nothing lost: nothing moves, nothing runs
         const int b = (int)(i & 1);
-        uint8_t* d_o = (uint8_t*)e->hslot[b].orig.p;
-        uint8_t* d_r = (uint8_t*)e->hslot[b].rec.p;
+        if (first_lane >= 0 && offset_pending && b != first_lane) {
+            RS16_HIP(hipStreamWaitEvent(e->hslot[b].s, e->hp_off, 0));
+            offset_pending = false;
+        }
+        auto& sl = e->hslot[b];
+        uint8_t* d_o = (uint8_t*)sl.orig.p;
+        uint8_t* d_r = (uint8_t*)sl.rec.p;
         uint8_t* d_of = (uint8_t*)e->hflags.p + b * (k + m);
         uint8_t* d_rf = d_of + k;
         const uint8_t* fo = original_received + i * original_received_stride;
         const uint8_t* fr = recovery_received + i * recovery_received_stride;
         uint8_t* ho = (uint8_t*)h_original + i * original_stride;
         const uint8_t* hr = (const uint8_t*)h_recovery + i * recovery_stride;
-        const bool work = ocnt[i] < k;  // (nothing lost: nothing moves, nothing runs)
-        // ---- in: flags and the received rows (after stripe i - 2's codec
-        // read them and its D2H read the originals restored in place there)
-        if (i >= 2) {
-            RS16_HIP(hipStreamWaitEvent(cin, ev[HP_CODEC][b], 0));
-            RS16_HIP(hipStreamWaitEvent(cin, ev[HP_D2H][b], 0));
+        // ---- in: the flags (through page-locked staging: a pageable source
+        // would make the copy synchronous; the lane's staging slot was last
+        // read by its previous stripe's copy) and the received rows
+        uint8_t* hf = (uint8_t*)e->hp_flags.p + b * (k + m);
+        RS16_HIP(hipEventSynchronize(ev[b]));
+        memcpy(hf, fo, k);
+        memcpy(hf + k, fr, m);
+        RS16_HIP(hipMemcpyAsync(d_of, hf, k + m, hipMemcpyHostToDevice, sl.s));
+        RS16_HIP(hipEventRecord(ev[b], sl.s));
+        if (int rc = copy_runs(fr, m, true, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
+                RS16_HIP(hipMemcpyAsync(d_r + r0 * S, hr + r0 * S, nr * S, hipMemcpyHostToDevice, sl.s));
+                return RS16_OK;
+            }))
+            return rc;
+        if (int rc = copy_runs(fo, k, true, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
+                RS16_HIP(hipMemcpyAsync(d_o + r0 * S, ho + r0 * S, nr * S, hipMemcpyHostToDevice, sl.s));
+                return RS16_OK;
+            }))
+            return rc;
+        if (first_lane < 0) {
+            RS16_HIP(hipEventRecord(e->hp_off, sl.s));
+            first_lane = b;
         }
-        if (work) {
-            // the flags go through page-locked staging (a pageable source
-            // would make the copy synchronous and stall the pipeline); the
-            // slot was last read by stripe i - 2's copy
-            uint8_t* hf = (uint8_t*)e->hp_flags.p + b * (k + m);
-            if (i >= 2) RS16_HIP(hipEventSynchronize(ev[HP_H2D][b]));
-            memcpy(hf, fo, k);
-            memcpy(hf + k, fr, m);
-            RS16_HIP(hipMemcpyAsync(d_of, hf, k + m, hipMemcpyHostToDevice, cin));
-            if (int rc = copy_runs(fr, m, true, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
-                    RS16_HIP(hipMemcpyAsync(d_r + r0 * S, hr + r0 * S, nr * S, hipMemcpyHostToDevice, cin));
-                    return RS16_OK;
-                }))
-                return rc;
-            if (int rc = copy_runs(fo, k, true, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
-                    RS16_HIP(hipMemcpyAsync(d_o + r0 * S, ho + r0 * S, nr * S, hipMemcpyHostToDevice, cin));
-                    return RS16_OK;
-                }))
-                return rc;
-        }
-        RS16_HIP(hipEventRecord(ev[HP_H2D][b], cin));
-        // ---- codec
-        RS16_HIP(hipStreamWaitEvent(cs, ev[HP_H2D][b], 0));
-        if (i >= 2) RS16_HIP(hipStreamWaitEvent(cs, ev[HP_D2H][b], 0));
-        if (work) {
+        // ---- codec, with the lane's own eval_poly outputs
+        {
+            EvalSet lane(e, b);
             DecodeGeom g = g0;
             g.a_recv = high ? rcnt[i] : ocnt[i];
             g.b_recv = high ? ocnt[i] : rcnt[i];
             const uint8_t* fa = high ? d_rf : d_of;
             const uint8_t* fb = high ? d_of : d_rf;
-            if (int rc = e->decode_eval(g, fa, fb, cs, err, S)) return rc;
-            if (int rc = e->decode_passes(g, S, S, high ? d_r : d_o, fa, high ? d_o : d_r, fb, d_o,
-                                          (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, cs,
-                                          err))
+            if (int rc = e->decode_eval(g, fa, fb, sl.s, err, S)) return rc;
+            if (int rc = e->decode_passes(g, S, S, high ? d_r : d_o, fa, high ? d_o : d_r, fb, d_o, (uint8_t*)sl.z.p,
+                                          (uint8_t*)sl.u.p, (uint32_t*)sl.rcount.p, sl.s, err))
                 return rc;
         }
-        RS16_HIP(hipEventRecord(ev[HP_CODEC][b], cs));
-        // ---- out: the restored originals only
-        RS16_HIP(hipStreamWaitEvent(cout, ev[HP_CODEC][b], 0));
-        if (work)
-            if (int rc = copy_runs(fo, k, false, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
-                    RS16_HIP(hipMemcpyAsync(ho + r0 * S, d_o + r0 * S, nr * S, hipMemcpyDeviceToHost, cout));
-                    return RS16_OK;
-                }))
-                return rc;
-        RS16_HIP(hipEventRecord(ev[HP_D2H][b], cout));
+        // ---- out: the restored originals (in place in the lane's rows)
+        if (int rc = copy_runs(fo, k, false, HP_MAX_RUNS, [&](size_t r0, size_t nr) -> int {
+                RS16_HIP(hipMemcpyAsync(ho + r0 * S, d_o + r0 * S, nr * S, hipMemcpyDeviceToHost, sl.s));
+                return RS16_OK;
+            }))
+            return rc;
     }
-    RS16_HIP(hipStreamSynchronize(cout));
-    RS16_HIP(hipStreamSynchronize(cin));
-    RS16_HIP(hipStreamSynchronize(cs));
-    if (int rc = e->scratch_done(cs, err)) return rc;
+    for (auto& sl : e->hslot) RS16_HIP(hipStreamSynchronize(sl.s));
+    if (int rc = e->scratch_done(e->stream, err)) return rc;
     e->forget_decode();  // (the counts came from the host flags: nothing for rs16_decode_check)
     return set_error(err, RS16_OK);
 }
@@ -1422,37 +1405,20 @@ static int note_flags_only(rs16_engine* e, const DecodeGeom& g, const uint8_t* f
     return set_error(err, RS16_OK);
 }
 
-extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, void* d_original,
-                                  const uint8_t* d_original_received, const void* d_recovery,
-                                  const uint8_t* d_recovery_received, size_t orig_recv, size_t rec_recv, void* stream,
-                                  rs16_error* err) {
-    bool high;
-    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
-    e->forget_decode();  // (whatever happens below, the previous decode is not checked again)
-    if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
-    if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
-    DecodeGeom g = decode_geom(high, k, m);
-    g.a_recv = high ? rec_recv : orig_recv;
-    g.b_recv = high ? orig_recv : rec_recv;
-    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
-    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
-    if (orig_recv == k) return note_flags_only(e, g, fl_a, fl_b, stream, err);
-    if (int rc = e->activate(err)) return rc;
-    hipStream_t s = e->pick(stream);
-    if (int rc = e->order(s, err)) return rc;
+// The passes of a device decode whose eval_poly is in ev_main (decode_eval
+// on stream s or a preparation ordered before s), per column slice.
+static int decode_device_passes(rs16_engine* e, const DecodeGeom& g, size_t S, void* d_original,
+                                const void* d_recovery, const uint8_t* fl_a, const uint8_t* fl_b, int n, hipStream_t s,
+                                rs16_error* err) {
     RS16_HIP(e->ws_z.reserve((size_t)g.n * S));
     RS16_HIP(e->ws_u.reserve((size_t)g.n * S));
     const uint8_t* orig = (const uint8_t*)d_original;
     const uint8_t* rec = (const uint8_t*)d_recovery;
-    const uint8_t* seg_a = high ? rec : orig;
-    const uint8_t* seg_b = high ? orig : rec;
-    // erasure logs once, then the passes per column slice on the slice streams
-    // (one slice: the column codec may compute them itself, decode_eval)
-    const int n = e->slice_count(S);
-    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, n == 1 ? S : 0)) return rc;
+    const uint8_t* seg_a = g.high ? rec : orig;
+    const uint8_t* seg_b = g.high ? orig : rec;
     if (n == 1) {
         if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
-                                      (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, s, err))
+                                      (uint8_t*)e->ws_u.p, (uint32_t*)e->ev_main.rcount.p, s, err))
             return rc;
         if (int rc = e->scratch_done(s, err)) return rc;
         return set_error(err, RS16_OK);
@@ -1472,6 +1438,90 @@ extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, 
     if (int rc = e->join(s, n, err)) return rc;
     if (int rc = e->scratch_done(s, err)) return rc;
     return set_error(err, RS16_OK);
+}
+
+extern "C" int rs16_decode_device(rs16_engine* e, size_t k, size_t m, size_t S, void* d_original,
+                                  const uint8_t* d_original_received, const void* d_recovery,
+                                  const uint8_t* d_recovery_received, size_t orig_recv, size_t rec_recv, void* stream,
+                                  rs16_error* err) {
+    bool high;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    e->forget_decode();  // (whatever happens below, the previous decode is not checked again)
+    if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
+    DecodeGeom g = decode_geom(high, k, m);
+    g.a_recv = high ? rec_recv : orig_recv;
+    g.b_recv = high ? orig_recv : rec_recv;
+    const uint8_t* fl_a = high ? d_recovery_received : d_original_received;
+    const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
+    if (orig_recv == k) return note_flags_only(e, g, fl_a, fl_b, stream, err);
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
+    // erasure logs once, then the passes per column slice on the slice streams
+    // (one slice: the column codec may compute them itself, decode_eval)
+    const int n = e->slice_count(S);
+    if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, n == 1 ? S : 0)) return rc;
+    return decode_device_passes(e, g, S, d_original, d_recovery, fl_a, fl_b, n, s, err);
+}
+
+// Split decode (include/rs16.h): the flag-dependent half of
+// rs16_decode_device -- validation and eval_poly of the received pattern
+// (src/rate/rate_high.rs:168-202, src/engine.rs:207-218) -- on one stream,
+// the passes on another.  The received pattern of a decode is known before
+// its shards are (a storage system knows which devices failed), so the
+// erasure locator can be computed while the shards are still being produced
+// or copied.  The preparation waits for the engine's earlier
+// work (a previous decode still reads the eval outputs) but does not become
+// the engine's last call: an encode issued after it on the engine stream runs
+// concurrently with it.
+extern "C" int rs16_decode_prepare(rs16_engine* e, size_t k, size_t m, size_t S, const uint8_t* d_original_received,
+                                   const uint8_t* d_recovery_received, size_t orig_recv, size_t rec_recv,
+                                   void* stream, rs16_error* err) {
+    bool high;
+    e->prep.valid = false;
+    if (int rc = resolve_rate(RS16_RATE_DEFAULT, k, m, S, &high, err)) return rc;
+    e->forget_decode();
+    if (orig_recv > k || rec_recv > m) return set_error(err, RS16_INVALID_ARGUMENT);
+    if (orig_recv + rec_recv < k) return set_error(err, RS16_NOT_ENOUGH_SHARDS, k, orig_recv, rec_recv);
+    rs16_engine::Prepared p;
+    p.k = k, p.m = m, p.S = S;
+    p.g = decode_geom(high, k, m);
+    p.g.a_recv = high ? rec_recv : orig_recv;
+    p.g.b_recv = high ? orig_recv : rec_recv;
+    p.fl_a = high ? d_recovery_received : d_original_received;
+    p.fl_b = high ? d_original_received : d_recovery_received;
+    p.nslices = e->slice_count(S);
+    p.nothing = orig_recv == k;
+    if (!p.nothing) {
+        if (int rc = e->activate(err)) return rc;
+        hipStream_t s = e->pick(stream);
+        if (int rc = e->order(s, err)) return rc;
+        if (int rc = e->guard_eval(s, false, err)) return rc;  // (an earlier, unconsumed preparation)
+        e->preparing = true;
+        const int rc = e->decode_eval(p.g, p.fl_a, p.fl_b, s, err, p.nslices == 1 ? S : 0);
+        e->preparing = false;
+        if (rc) return rc;
+        if (!e->prep_ev) RS16_HIP(hipEventCreateWithFlags(&e->prep_ev, hipEventDisableTiming));
+        RS16_HIP(hipEventRecord(e->prep_ev, s));
+        e->prep_pending = true;
+    }
+    p.valid = true;
+    e->prep = p;
+    return set_error(err, RS16_OK);
+}
+
+extern "C" int rs16_decode_device_prepared(rs16_engine* e, size_t k, size_t m, size_t S, void* d_original,
+                                           const void* d_recovery, void* stream, rs16_error* err) {
+    const rs16_engine::Prepared p = e->prep;
+    if (!p.valid || p.k != k || p.m != m || p.S != S) return set_error(err, RS16_INVALID_ARGUMENT);
+    e->prep.valid = false;
+    if (p.nothing) return note_flags_only(e, p.g, p.fl_a, p.fl_b, stream, err);
+    if (int rc = e->activate(err)) return rc;
+    hipStream_t s = e->pick(stream);
+    if (int rc = e->order(s, err)) return rc;
+    if (int rc = e->guard_eval(s, true, err)) return rc;  // after the preparation's eval_poly
+    return decode_device_passes(e, p.g, S, d_original, d_recovery, p.fl_a, p.fl_b, p.nslices, s, err);
 }
 
 // rs16_decode_device for nstripes independent stripes that lost the same
@@ -1517,7 +1567,7 @@ extern "C" int rs16_decode_device_batch(rs16_engine* e, size_t k, size_t m, size
     const uint8_t* fl_b = high ? d_original_received : d_recovery_received;
     if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, S, nstripes)) return rc;
     if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, (uint8_t*)d_original, (uint8_t*)e->ws_z.p,
-                                  (uint8_t*)e->ws_u.p, (uint32_t*)e->ws_rcount.p, s, err, nstripes, bs_a, bs_b,
+                                  (uint8_t*)e->ws_u.p, (uint32_t*)e->evset->rcount.p, s, err, nstripes, bs_a, bs_b,
                                   original_stride))
         return rc;
     if (int rc = e->scratch_done(s, err)) return rc;
@@ -1593,7 +1643,7 @@ extern "C" int rs16_decode_device_batch_varied(rs16_engine* e, size_t k, size_t 
         const uint32_t vary = ns > 1 ? (uint32_t)ns : 0;
         if (int rc = e->decode_eval(g, fl_a, fl_b, s, err, S, ns, vary, fs_a, fs_b)) return rc;
         if (int rc = e->decode_passes(g, S, S, seg_a, fl_a, seg_b, fl_b, og, (uint8_t*)e->ws_z.p, (uint8_t*)e->ws_u.p,
-                                      (uint32_t*)e->ws_rcount.p, s, err, ns, bs_a, bs_b, original_stride))
+                                      (uint32_t*)e->evset->rcount.p, s, err, ns, bs_a, bs_b, original_stride))
             return rc;
     }
     e->forget_decode();

@@ -237,7 +237,7 @@ ColArgs rs16_engine::col_args() const {
     a.skew_tab = d_skew_tab;
     a.mul_tab = d_mul_tab;
     a.zero = d_zero_sink;
-    a.elog = (const uint32_t*)ws_elog.p;
+    a.elog = (const uint32_t*)evset->elog.p;
     a.nstripes = 1;
     a.diag = (uint32_t)diag;
     return a;
@@ -432,19 +432,30 @@ int rs16_engine::decode_fused(const DecodeGeom& g, size_t S, size_t S_user, cons
                               const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                               hipStream_t s, rs16_error* err) {
     if (int rc = decode_eval(g, flags_a, flags_b, s, err, S)) return rc;
-    return decode_passes(g, S, S_user, seg_a, flags_a, seg_b, flags_b, rest, Z, U, (uint32_t*)ws_rcount.p, s, err);
+    return decode_passes(g, S, S_user, seg_a, flags_a, seg_b, flags_b, rest, Z, U, (uint32_t*)evset->rcount.p, s, err);
 }
 
-// Erasure logs e = eval_poly(erasure vector) into ws_elog (2-3 small kernels).
+int rs16_engine::guard_eval(hipStream_t s, bool consume, rs16_error* err) {
+    if (!prep_pending) return RS16_OK;
+    RS16_HIP(hipStreamWaitEvent(s, prep_ev, 0));
+    prep_pending = false;
+    if (!consume) prep.valid = false;
+    return RS16_OK;
+}
+
+// Erasure logs e = eval_poly(erasure vector) into evset->elog (2-3 small kernels).
 int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
                              rs16_error* err, size_t S, size_t nstripes, uint32_t vary, size_t bs_fa, size_t bs_fb) {
+    // (a prepared decode's outputs in ev_main are about to be overwritten)
+    if (evset == &ev_main && !preparing)
+        if (int rc = guard_eval(s, false, err)) return rc;
     const size_t nv = vary > 1 ? vary : 1;
-    RS16_HIP(ws_work32.reserve(nv * VARY_WORK * 4));
-    RS16_HIP(ws_elog.reserve(nv * VARY_WORK * 4));
-    RS16_HIP(ws_zflag.reserve(nv * VARY_ZFLAGS));
-    RS16_HIP(ws_rbits.reserve(nv * VARY_RBITS * 4));
-    RS16_HIP(ws_lost.reserve(nv * VARY_LOST * 4));
-    RS16_HIP(ws_rcount.reserve(GF_ORDER / 64 * 8));
+    RS16_HIP(evset->work32.reserve(nv * VARY_WORK * 4));
+    RS16_HIP(evset->elog.reserve(nv * VARY_WORK * 4));
+    RS16_HIP(evset->zflag.reserve(nv * VARY_ZFLAGS));
+    RS16_HIP(evset->rbits.reserve(nv * VARY_RBITS * 4));
+    RS16_HIP(evset->lost.reserve(nv * VARY_LOST * 4));
+    RS16_HIP(evset->rcount.reserve(GF_ORDER / 64 * 8));
     var_ns = vary > 1 ? vary : 0;
     var_bs_fa = vary > 1 ? bs_fa : 0;
     var_bs_fb = vary > 1 ? bs_fb : 0;
@@ -459,17 +470,17 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // the pass metadata: received bitmap, and zero flags of the first pass's
     // tiles (2^lo rows, lo = L/2) when the decode takes more than one pass
     const int L = ilog2(g.n);
-    es.rbits = (uint32_t*)ws_rbits.p;
-    es.zflags = L > 8 ? (uint8_t*)ws_zflag.p : nullptr;
+    es.rbits = (uint32_t*)evset->rbits.p;
+    es.zflags = L > 8 ? (uint8_t*)evset->zflag.p : nullptr;
     es.n = g.n;
     es.zlo = (uint32_t)(L / 2);
     // the lost originals' row range prunes the general multi-pass decode
     // (the half-transform decode restores every original: not needed)
     const bool prune = !half_decode(g) && L > 8;
-    es.lostpart = prune ? (uint32_t*)ws_lost.p : nullptr;
-    es.lostrange = prune ? (uint32_t*)ws_lost.p + 512 : nullptr;
+    es.lostpart = prune ? (uint32_t*)evset->lost.p : nullptr;
+    es.lostrange = prune ? (uint32_t*)evset->lost.p + 512 : nullptr;
     es.orig_b = g.high ? 1 : 0;
-    es.rcount = (uint32_t*)ws_rcount.p;
+    es.rcount = (uint32_t*)evset->rcount.p;
     es.diag = (uint32_t)diag;
     last_dec = g;
     last_dec_valid = true;
@@ -493,8 +504,8 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
                                        : col_ok(ilog2(g.n), S, nstripes, true));
     if (eval_in_col) return RS16_OK;
     es.stamps = stamp_prof == PROF_EVAL_POLY ? (uint64_t*)stamp_buf : nullptr;
-    hipEvent_t ev;
-    if (int rc = prof_begin(s, &ev, err)) return rc;
+    hipEvent_t pev;
+    if (int rc = prof_begin(s, &pev, err)) return rc;
     // The decode passes that read erasure logs finish eval_poly's last
     // 256-point FWHT themselves, for the 256-row block of their tile's rows
     // (one kernel less) -- except the one-pass half-transform decode, whose
@@ -504,13 +515,13 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     elog_fused = !(half_decode(g) && ilog2(g.n) - 1 <= 8);
     if (small) {
         // erasures are zero from row n on: only n/256 live blocks (rs16_misc.hip)
-        RS16_HIP(launch_eval_poly_small(es, (uint32_t)g.n, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh,
+        RS16_HIP(launch_eval_poly_small(es, (uint32_t)g.n, (uint32_t*)evset->work32.p, (uint32_t*)evset->elog.p, d_log_walsh,
                                         s, !elog_fused));
     } else {
-        RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)ws_work32.p, (uint32_t*)ws_elog.p, d_log_walsh, s,
+        RS16_HIP(launch_eval_poly_from_flags(es, (uint32_t*)evset->work32.p, (uint32_t*)evset->elog.p, d_log_walsh, s,
                                              !elog_fused));
     }
-    return prof_end(PROF_EVAL_POLY, s, ev, err);
+    return prof_end(PROF_EVAL_POLY, s, pev, err);
 }
 
 // Half-transform decode.  When every original is lost and the originals'
@@ -530,8 +541,8 @@ bool rs16_engine::half_decode(const DecodeGeom& g) {
     return orig_lost && g.n >= 2 && g.n == 2 * (size_t)g.chunk;
 }
 
-// The pass sequence of a decode, given what decode_eval left in ws_elog /
-// ws_work32 (erasure logs), ws_rbits (received rows) and ws_zflag (zero tiles).
+// The pass sequence of a decode, given what decode_eval left in evset->elog /
+// evset->work32 (erasure logs), evset->rbits (received rows) and evset->zflag (zero tiles).
 int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
                                const uint8_t* seg_b, const uint8_t* flags_b, uint8_t* rest, uint8_t* Z, uint8_t* U,
                                uint32_t* rcount, hipStream_t s, rs16_error* err, size_t nst, size_t bs_a, size_t bs_b,
@@ -545,11 +556,11 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.a_count = g.a_count;
     a.chunk = g.chunk;
     a.b_count = g.b_count;
-    a.elog = (const uint32_t*)ws_elog.p;
-    a.ework = elog_fused ? (const uint32_t*)ws_work32.p : nullptr;
+    a.elog = (const uint32_t*)evset->elog.p;
+    a.ework = elog_fused ? (const uint32_t*)evset->work32.p : nullptr;
     a.rest = rest;
     a.rest_seg_b = g.high ? 1 : 0;
-    a.rbits = (const uint32_t*)ws_rbits.p;
+    a.rbits = (const uint32_t*)evset->rbits.p;
     a.skew_ifft = a.skew_fft = 0;
     if (var_ns) {  // stripes with losses of their own (decode_eval's per-stripe metadata)
         a.bs_fa = var_bs_fa;
@@ -619,7 +630,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
                 c.rcount = rcount;
                 return col(c, Lh, COL_DEC_EVAL, s, err);
             }
-            c.elog = (const uint32_t*)ws_work32.p;  // (eval_poly without its last H_lo: elog_fused)
+            c.elog = (const uint32_t*)evset->work32.p;  // (eval_poly without its last H_lo: elog_fused)
             return col(c, Lh, COL_DEC_EWORK, s, err);
         }
         const int lo = Lh / 2, hi = Lh - lo;
@@ -671,8 +682,8 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     const int lo = L / 2, hi = L - lo;
     // One flag per DEC_FIRST tile (2^hi <= 256): tiles without a received
     // row are skipped by DEC_FIRST and read as zero by DEC_MID / DEC_LAST.
-    a.zflags = (const uint8_t*)ws_zflag.p;
-    a.lostrange = (const uint32_t*)ws_lost.p + 512;  // (written by decode_eval)
+    a.zflags = (const uint8_t*)evset->zflag.p;
+    a.lostrange = (const uint32_t*)evset->lost.p + 512;  // (written by decode_eval)
     // Launch only the tiles that can hold a received row: a segment with no
     // received shard contributes none (its tiles are flagged by block 0).
     const uint32_t tile = 1u << lo, ntiles = 1u << hi;
@@ -715,6 +726,7 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         const uint32_t tiles = batch(t1 - t0, zs, zs, 0);
         hipEvent_t ev;
         if (int rc = prof_begin(s, &ev, err)) return rc;
+        if (stamp_buf && stamp_prof == DEC_LAST) a.stamps = (uint64_t*)stamp_buf;
         RS16_HIP(launch_tile_last(a, tiles, s));
         return prof_end(DEC_LAST, s, ev, err);
     }

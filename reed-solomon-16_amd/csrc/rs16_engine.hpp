@@ -81,11 +81,40 @@ struct rs16_engine {
     uint16_t* d_log_walsh = nullptr;
     uint8_t* d_zero_sink = nullptr;  // zero page (PassArgs::zero, ColArgs::zero)
     // scratch
-    rs16::DevBuf ws_z, ws_u, ws_fd, ws_work32, ws_elog, ws_flags;
-    rs16::DevBuf ws_zflag;  // decode: per DEC_FIRST tile, 1 = no received row (tile skipped, rows zero)
-    rs16::DevBuf ws_rbits;  // decode: received-row bitmap (65536 bits)
-    rs16::DevBuf ws_lost;   // decode: lost-original row range per 256-row block (2 KiB) + overall (8 B)
-    rs16::DevBuf ws_rcount; // decode: received rows per 64-row chunk and segment (ErasureSpec::rcount)
+    rs16::DevBuf ws_z, ws_u, ws_fd, ws_flags;
+    // The decode's eval_poly outputs / pass metadata (written by decode_eval,
+    // read by decode_passes).  `evset` points at the set the next decode uses:
+    // ev_main, or one of the pipelined host path's per-lane sets (so that
+    // two lanes' decodes never share them).
+    struct EvalBufs {
+        rs16::DevBuf work32, elog;
+        rs16::DevBuf zflag;   // per DEC_FIRST tile, 1 = no received row (tile skipped, rows zero)
+        rs16::DevBuf rbits;   // received-row bitmap (65536 bits)
+        rs16::DevBuf lost;    // lost-original row range per 256-row block (2 KiB) + overall (8 B)
+        rs16::DevBuf rcount;  // received rows per 64-row chunk and segment (ErasureSpec::rcount)
+        void release() { work32.release(), elog.release(), zflag.release(), rbits.release(), lost.release(), rcount.release(); }
+    };
+    EvalBufs ev_main, ev_lane[2];
+    EvalBufs* evset = &ev_main;
+    // Split decode (rs16_decode_prepare / rs16_decode_device_prepared): the
+    // prepared received pattern, whose eval_poly went to ev_main on the
+    // prepare's stream; prep_ev marks its end.  While prep_pending, any other
+    // use of ev_main first orders itself after prep_ev (guard_eval).
+    struct Prepared {
+        bool valid = false, nothing = false;
+        size_t k = 0, m = 0, S = 0;
+        rs16::DecodeGeom g{};
+        const uint8_t* fl_a = nullptr;
+        const uint8_t* fl_b = nullptr;
+        int nslices = 1;
+    } prep;
+    hipEvent_t prep_ev = nullptr;
+    bool prep_pending = false;
+    bool preparing = false;
+    // order stream s after a pending preparation's eval_poly (whose outputs
+    // the caller is about to overwrite or read) and drop the preparation
+    // unless it is the one being consumed
+    int guard_eval(hipStream_t s, bool consume, rs16_error* err);
     // the last decode's geometry and the received counts it was given (rs16_decode_check)
     rs16::DecodeGeom last_dec{};
     bool last_dec_valid = false;
@@ -123,9 +152,10 @@ struct rs16_engine {
     int join(hipStream_t s, int n, rs16_error* err);
     rs16::DevBuf hflags;
     hipEvent_t hev = nullptr;
-    // pipelined host stripes (rs16_{en,de}code_host_batch): per buffer parity,
-    // H2D done / codec done / D2H done
-    hipEvent_t hp_ev[3][2] = {};
+    // pipelined host stripes (rs16_{en,de}code_host_batch): per lane, the
+    // flag bytes' copy out of hp_flags is done
+    hipEvent_t hp_ev[2] = {};
+    hipEvent_t hp_off = nullptr;  // the first stripe's H2D is done: the other lane's first H2D starts then
     rs16::HostBuf hp_flags;  // page-locked staging of the decode's flag bytes (2 x (k + m))
     int host_pipe_events(rs16_error* err);
     int host_slots(rs16_error* err);

@@ -1492,6 +1492,7 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
         const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
         if (!((tile << T) < r1 && ((tile + 1) << T) > r0)) return;
     }
+    RS16_STAMP(a, 0);
     const uint32_t q = qg * 4 + w;
     const bool active = q < a.qrow;
     const uint32_t offL = (q >> 3) * 64 + (q & 7) * 4;
@@ -1532,6 +1533,7 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
                                              (colops::lds_vp)(tabs + (i * 256 + 64 * w) * 16), 16, 0, 0);
         }
     }
+    RS16_STAMP(a, 1);
     __builtin_amdgcn_s_waitcnt(0);
     if (a.ework && w == 0) {
         fwht256_wave(ev);  // the last 256-point FWHT of eval_poly (src/engine.rs:207-218)
@@ -1539,6 +1541,7 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
         for (int j = 0; j < 4; j++) elds[lane + 64 * j] = ev[j];
     }
     __syncthreads();  // tables and logs in LDS
+    RS16_STAMP(a, 2);
     // ---- reveal multipliers of the lane's output rows (the last block's
     // layout: row k = 4 lane + m), requested now, used after the FFT
     uint32_t rt[4][20];
@@ -1590,6 +1593,7 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
     using I5 = std::integral_constant<int, 5>;
     using I6 = std::integral_constant<int, 6>;
     using I7 = std::integral_constant<int, 7>;
+    RS16_STAMP(a, 3);
     BlockTabs ta, tb;
     tabs_of(ta, I6(), I7());
     tabs_of(tb, I4(), I5());
@@ -1602,6 +1606,7 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
     compute<true, true, true>(YL, YH, ta);
     wave_exchange<0, 1>(YL, YH);
     compute<true, true, true>(YL, YH, tb);
+    RS16_STAMP(a, 9);
     // ---- reveal (x (65535 - e)) and store the lost originals in place
     // (restored-originals row = work row - the originals' segment start)
     const int64_t shift = (int64_t)a.row_base_out - (a.rest_seg_b ? (int64_t)a.chunk : 0);
@@ -1617,6 +1622,8 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
         p[0] = ol;
         p[8] = oh;
     }
+    RS16_STAMP(a, 10);
+    RS16_STAMP_END(a);
 }
 
 hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s) {

@@ -30,7 +30,7 @@ __all__ = [
     "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS", "set_diagnostics",
     "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL", "DIAG_NO_COLUMN", "DIAG_FORCE_COLUMN",
     "DIAG_TILE_LAST", "DIAG_NO_TILE_LAST", "DIAG_FD_LDS", "DIAG_COL_RADIX4", "encode_host", "decode_host",
-    "encode_host_batch", "decode_host_batch",
+    "encode_host_batch", "decode_host_batch", "decode_prepare", "decode_device_prepared",
     "encode_host_multi", "decode_host_multi", "Comm", "column_slice", "scatter_columns", "gather_columns",
 ]
 
@@ -687,6 +687,30 @@ def decode_device(original_count, recovery_count, shard_bytes, d_original, d_ori
                                     Engine._ptr(d_original_received), Engine._ptr(d_recovery),
                                     Engine._ptr(d_recovery_received), original_received_count,
                                     recovery_received_count, stream, C.byref(err)), err)
+    if check:
+        _check(lib().rs16_decode_check(eng.h, stream, C.byref(err)), err)
+
+
+def decode_prepare(original_count, recovery_count, shard_bytes, d_original_received, d_recovery_received,
+                   original_received_count, recovery_received_count, stream=None, engine: Optional[Engine] = None):
+    """rs16_decode_prepare: the erasure locator of a received pattern on
+    `stream`, ahead of the shards (see decode_device_prepared)."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_decode_prepare(eng.h, original_count, recovery_count, shard_bytes,
+                                     Engine._ptr(d_original_received), Engine._ptr(d_recovery_received),
+                                     original_received_count, recovery_received_count, stream, C.byref(err)), err)
+
+
+def decode_device_prepared(original_count, recovery_count, shard_bytes, d_original, d_recovery, stream=None,
+                           engine: Optional[Engine] = None, check: bool = False):
+    """rs16_decode_device_prepared: the rest of the decode prepared last on this
+    engine (same results as decode_device)."""
+    eng = engine or default_engine()
+    err = RS16Error()
+    _check(lib().rs16_decode_device_prepared(eng.h, original_count, recovery_count, shard_bytes,
+                                             Engine._ptr(d_original), Engine._ptr(d_recovery), stream, C.byref(err)),
+           err)
     if check:
         _check(lib().rs16_decode_check(eng.h, stream, C.byref(err)), err)
 

@@ -105,6 +105,8 @@ SIGNATURES = {
     "rs16_scatter_columns_virtual": (_i, [_p, _i, _sz, _sz, _p, _p, _p, _e]),
     "rs16_gather_columns_virtual": (_i, [_p, _i, _sz, _sz, _p, _p, _p, _e]),
     "rs16_encode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _e]),
+    "rs16_decode_prepare": (_i, [_p, _sz, _sz, _sz, _p, _p, _sz, _sz, _p, _e]),
+    "rs16_decode_device_prepared": (_i, [_p, _sz, _sz, _sz, _p, _p, _p, _e]),
     "rs16_encode_host_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _sz, _e]),
     "rs16_decode_host_batch": (_i, [_p, _sz, _sz, _sz, _sz, _p, _sz, _p, _sz, _p, _sz, _p, _sz, _e]),
     "rs16_decode_host_multi": (_i, [_p, _i, _sz, _sz, _sz, _p, _p, _p, _p, _e]),
