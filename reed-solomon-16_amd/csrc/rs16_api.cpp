@@ -144,7 +144,7 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
 extern "C" int rs16_engine_set_diagnostics(rs16_engine* e, int flags) {
     const int old = e->diag;
     e->diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN |
-                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4);
+                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4 | DIAG_NO_IDENTITY);
     return old;
 }
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
@@ -1428,10 +1428,12 @@ static int decode_device_passes(rs16_engine* e, const DecodeGeom& g, size_t S, v
     for (int j = 0, b0 = 0; j < n; j++) {
         const size_t b1 = blocks * (j + 1) / n, off = b0 * 64, w = (b1 - b0) * 64;
         // (decode_eval was told the slices are narrower than S: no column
-        // decode evaluates the polynomial itself, nothing writes rcount here)
+        // decode evaluates the polynomial itself; with identity multipliers
+        // the first slice's passes count the received rows)
+        uint32_t* rc_j = j == 0 && e->e_ident ? (uint32_t*)e->ev_main.rcount.p : nullptr;
         if (int rc = e->decode_passes(g, w, S, seg_a + off, fl_a, seg_b + off, fl_b, (uint8_t*)d_original + off,
                                       (uint8_t*)e->ws_z.p + (size_t)g.n * off, (uint8_t*)e->ws_u.p + (size_t)g.n * off,
-                                      nullptr, e->sl_stream[j], err))
+                                      rc_j, e->sl_stream[j], err))
             return rc;
         b0 = (int)b1;
     }

@@ -497,6 +497,13 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
         es.rcount = nullptr;
         last_dec_valid = false;
     }
+    // A whole-half erasure: every log is 0, nothing to evaluate (the passes
+    // count the received rows for rs16_decode_check)
+    e_ident = identity_logs(g, vary);
+    if (e_ident) {
+        eval_in_col = elog_fused = false;
+        return RS16_OK;
+    }
     // High-rate half decodes of 2^9 / 2^10-row halves through the column
     // codec: it evaluates the polynomial itself (an n-point XOR convolution,
     // rs16_col.hip) and writes rcount; no kernel here.
@@ -539,6 +546,25 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
 bool rs16_engine::half_decode(const DecodeGeom& g) {
     const bool orig_lost = g.high ? g.b_recv == 0 : g.a_recv == 0;
     return orig_lost && g.n >= 2 && g.n == 2 * (size_t)g.chunk;
+}
+
+// Identity multipliers.  When the erased rows are exactly one half of the n
+// = 2^(L+1) work rows and the other half is received whole (k = m = n / 2,
+// every original lost, every recovery shard received; the low rate adds the
+// tail [n, 65536), rate_low.rs:183-197), the erasure log of every work row,
+// eval_poly(e)[i] = sum_{j erased} log(i ^ j) mod 65535 (src/engine.rs:207-218
+// as an XOR convolution with H(LogWalsh) = log), is the log of the
+// subspace polynomial of the erased half at i: 0 for every i (the Cantor
+// basis normalizes it to 1 on the complementary coset; checked against the
+// oracle for every L in tests/test_eval_identity.py).  Then "MULTIPLY
+// SHARDS" (rate_high.rs:203-228) and REVEAL ERASURES (:236-242) multiply by
+// exp(0) = 1 and exp(65535) = 1: the passes take the rows as they are.  Only
+// the pass form of the half decode (halves of 2^11 rows and more) uses it;
+// the counts the caller gave pick it, as they pick the half decode.
+bool rs16_engine::identity_logs(const DecodeGeom& g, uint32_t vary) const {
+    if ((diag & DIAG_NO_IDENTITY) || vary > 1 || !half_decode(g) || ilog2(g.n) - 1 < 11) return false;
+    if (g.a_count != g.chunk || g.b_count != g.chunk) return false;
+    return g.high ? g.a_recv == g.a_count : g.b_recv == g.b_count;
 }
 
 // The pass sequence of a decode, given what decode_eval left in evset->elog /
@@ -594,6 +620,37 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
         a.row_base_in = a.skew_ifft = src;
         a.row_base_out = a.skew_fft = dst;
         const int Lh = L - 1;
+        if (e_ident) {
+            // Identity multipliers (identity_logs): gather the received half
+            // as it is -> IFFT -> FFT -> its rows are the restored originals,
+            // i.e. the encoder's three passes with the half's twiddles; the
+            // first and last count the received flags for rs16_decode_check
+            const int lo = Lh / 2, hi = Lh - lo;
+            a.seg_a = g.high ? seg_a : seg_b;
+            a.bs_seg = g.high ? bs_a : bs_b;
+            a.a_count = half;
+            a.rcount = rcount;
+            a.cnt_flags = g.high ? flags_a : flags_b;
+            a.cnt_base = src;
+            a.cnt_seg = g.high ? 0 : 1;
+            a.lo = 0;
+            a.out = Z;
+            RS16_PASS_AS(PROF_DEC_HALF_FIRST, ENC_FIRST, lo, a, batch(1u << hi, 0, 0, zs), s);
+            a.rcount = nullptr;
+            a.lo = lo;
+            a.in = Z;
+            RS16_PASS_AS(PROF_DEC_HALF_MID, ENC_MID, hi, a, batch(1u << lo, zs, 0, zs), s);
+            a.lo = 0;
+            a.out = rest;
+            a.S_out = S_user;
+            a.out_rows = orig;
+            a.rcount = rcount;
+            a.cnt_flags = g.high ? flags_b : flags_a;
+            a.cnt_base = dst;
+            a.cnt_seg = g.high ? 1 : 0;
+            RS16_PASS_AS(DEC_HALF_LAST, ENC_LAST, lo, a, batch((orig + (1u << lo) - 1) >> lo, zs, 0, bs_rest), s);
+            return RS16_OK;
+        }
         // 2^6 .. 2^10-row halves: the whole decode in one launch (rs16_col.hip)
         // -- high rate with the polynomial in the kernel; the low rate from
         // 2^9 rows on, on eval_poly's output

@@ -198,6 +198,7 @@ struct rs16_engine {
     int stamp_prof = -1;
     bool elog_fused = false;  // last decode_eval left the final 256-point FWHT to the passes (ws_work32)
     bool eval_in_col = false; // last decode_eval left eval_poly to the column codec (COL_DEC_EVAL)
+    bool e_ident = false;     // last decode_eval found every erasure log 0 (identity_logs): no eval_poly kernel
     struct ProfRec {
         int id;
         hipEvent_t a, b;
@@ -233,6 +234,9 @@ struct rs16_engine {
     // flags at flags_a / flags_b + i bs_fa / bs_fb bytes: one grid row of the
     // eval kernels per stripe, per-stripe metadata (VARY_* strides below),
     // which the decode_passes that follow read (var_* state).
+    // Every erasure log of the decode is 0 (a whole-half erasure, DESIGN.md
+    // 3.13): the multipliers are identities and eval_poly is not launched.
+    bool identity_logs(const rs16::DecodeGeom& g, uint32_t vary) const;
     int decode_eval(const rs16::DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
                     rs16_error* err, size_t S = 0, size_t nstripes = 1, uint32_t vary = 0, size_t bs_fa = 0,
                     size_t bs_fb = 0);

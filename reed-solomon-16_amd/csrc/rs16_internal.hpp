@@ -178,6 +178,17 @@ struct PassArgs {
     uint32_t bs_elog, bs_rbits, bs_zflags, bs_lost;
     // the engine's diagnostic switches (DiagFlags; host side: launch_pass)
     uint32_t diag;
+    // ENC_FIRST / ENC_LAST as the passes of a decode with identity erasure
+    // multipliers (rs16_engine::identity_logs): no eval_poly kernel read the
+    // received flags, so these passes count them for rs16_decode_check.  Pass
+    // row r (< 2^L of the half this launch covers) is decode work row r +
+    // cnt_base with flag byte cnt_flags[r] (nullptr: received); the received
+    // count of each 64-row chunk goes to rcount[2 (row >> 6) + cnt_seg] and 0
+    // to the other segment's slot (ErasureSpec::rcount layout).  rcount
+    // nullptr: not counted.
+    uint32_t* rcount;
+    const uint8_t* cnt_flags;
+    uint32_t cnt_base, cnt_seg;
 };
 
 // One-launch codec for 2^9 / 2^10-row transforms (rs16_col.hip): one
@@ -264,6 +275,7 @@ enum DiagFlags : int {
     DIAG_NO_TILE_LAST = 64,   // ... always as the 8-wave pass (DEC_LAST items)
     DIAG_FD_LDS = 128,        // DEC_MID's in-tile formal derivative always through the LDS image (tile_fd)
     DIAG_COL_RADIX4 = 256,    // column codec: the 4-rows-per-thread form for every transform (col_kernel)
+    DIAG_NO_IDENTITY = 512,   // whole-half erasures: eval_poly and the per-row multipliers anyway (identity_logs)
 };
 
 constexpr size_t RS16_ZERO_BYTES = 65536;

@@ -1090,6 +1090,42 @@ template <int P, int T> struct TileStage {
     }
 };
 
+// Received counts of a decode with identity multipliers (PassArgs::rcount,
+// ENC_FIRST / ENC_LAST launched by decode_passes): wave j of the first
+// slab's workgroup counts chunk j of its tile (a tile below 64 rows: the
+// chunk's first tile counts it).  Behind uniform branches: the flag bytes
+// are the workgroup's first loads (so the compiler's waits for the later
+// loads do not change), the ballots run after the staging barrier (the bytes
+// are older than the tables it waited for) and the counts, in SGPRs, are
+// stored after the item.
+template <int P, int T> struct RcvCount {
+    static constexpr bool ON = P == ENC_FIRST || P == ENC_LAST;
+    static constexpr uint32_t NCH = (1u << T) >= 64 ? (1u << T) / 64 : 1;
+    bool go;
+    uint32_t r0, f, cnt;
+    __device__ __forceinline__ void issue(const PassArgs& a, const Thr& c, bool first) {
+        go = false;
+        if constexpr (ON) {
+            r0 = uni(row_rel<T>(c, a, 0) + 64u * c.w);
+            go = first && a.rcount && c.w < NCH && (r0 & 63u) == 0;
+            if (go) f = !a.cnt_flags || a.cnt_flags[r0 + c.lane];
+        }
+    }
+    __device__ __forceinline__ void count() {
+        if constexpr (ON)
+            if (go) cnt = uni((uint32_t)__popcll(__ballot(f != 0)));
+    }
+    __device__ __forceinline__ void store(const PassArgs& a, const Thr& c) const {
+        if constexpr (ON) {
+            if (go && c.lane == 0) {
+                const uint32_t ch = (r0 + a.cnt_base) >> 6;
+                a.rcount[2 * ch + a.cnt_seg] = cnt;
+                a.rcount[2 * ch + 1 - a.cnt_seg] = 0;
+            }
+        }
+    }
+};
+
 // Compute and store one item whose rows are in d (every thread of the
 // workgroup calls it for the same item).
 // The one-item build's store of row register m of an item (the counterpart
@@ -1368,9 +1404,11 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     uint32_t tile, slab;
     set_item(c, a, item, G::Q, tile, slab);
 
+    bool first_stripe = true;
     if (a.stripe_tiles) {
         // batched stripes: the stripe's arrays, the tile within the stripe
         const uint32_t st = uni(tile / a.stripe_tiles);
+        first_stripe = st == 0;
         tile -= st * a.stripe_tiles;
         a.in += st * a.bs_in;
         a.in2 += st * a.bs_in2;
@@ -1391,6 +1429,8 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     tile += a.tile_base;
     c.b_low = tile & ((1u << a.lo) - 1);
     c.b_high = tile >> a.lo;
+    RcvCount<P, T> rcn;
+    rcn.issue(a, c, slab == 0 && first_stripe);
     if constexpr (P == DEC_FIRST) {
         // a tile without received rows is skipped (process_item): return
         // before its table staging and row loads, so its slot frees at once
@@ -1443,8 +1483,10 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
     RS16_STAMP(a, 1);
     prio<P, 0, T>();
     st.template finish<EARLY>(a, c, smem);
+    rcn.count();
     RS16_STAMP(a, 2);
     process_item<P, T>(a, c, tile, slab, cur, smem);
+    rcn.store(a, c);
 }
 
 // ---------------------------------------------------------------------------

@@ -21,7 +21,7 @@ On top of that every case draws what this engine's path choice depends on:
   * the engine's diagnostic switches (rs16_engine_set_diagnostics), each on
     with probability 0.15: forced column / pass codec, radix-4 column form,
     64-bit lane offsets, the eval_poly forms, the last-pass forms, the
-    formal derivative through LDS.
+    formal derivative through LDS, the evaluated erasure logs of whole-half erasures.
 Every case's parameters are in the assertion message.
 """
 import numpy as np
@@ -35,7 +35,7 @@ pytestmark = pytest.mark.gpu
 GF_ORDER = 65536
 DIAGS = (rs16.DIAG_FORCE_VOFF64, rs16.DIAG_EVAL_TWO_KERNEL, rs16.DIAG_EVAL_FULL, rs16.DIAG_NO_COLUMN,
          rs16.DIAG_FORCE_COLUMN, rs16.DIAG_TILE_LAST, rs16.DIAG_NO_TILE_LAST, rs16.DIAG_FD_LDS,
-         rs16.DIAG_COL_RADIX4)
+         rs16.DIAG_COL_RADIX4, rs16.DIAG_NO_IDENTITY)
 BUDGET = 3 << 20  # bytes of originals + recovery per case (all stripes)
 
 
