@@ -5,9 +5,12 @@ def short(n):
     m = re.search(r"pass_kernel<(\d+), (\d+)>", n)
     progs = ["GEN_FFT","GEN_IFFT","ENC_FIRST","ENC_MID","ENC_LAST","ENC_SINGLE","DEC_FIRST","DEC_MID","DEC_LAST",
              "DEC_SINGLE","DEC_HALF_LAST","DEC_HALF_SINGLE"]
-    # the half-transform decode runs DEC_FIRST (T7) as DEC_HALF_FIRST and
-    # ENC_MID (T8) as DEC_HALF_MID: those rows average both uses
-    alias = {("ENC_MID", "8"): "ENC_MID+DEC_HALF_MID", ("DEC_FIRST", "7"): "DEC_HALF_FIRST"}
+    # the half-transform decode runs ENC_MID (T8) as DEC_HALF_MID, and with
+    # identity multipliers (the bench step) ENC_FIRST / ENC_LAST
+    # (T7) as DEC_HALF_FIRST / DEC_HALF_LAST: those rows average both uses;
+    # the evaluated half decode runs DEC_FIRST (T7) as DEC_HALF_FIRST
+    alias = {("ENC_MID", "8"): "ENC_MID+DEC_HALF_MID", ("ENC_FIRST", "7"): "ENC_FIRST+DEC_HALF_FIRST",
+             ("ENC_LAST", "7"): "ENC_LAST+DEC_HALF_LAST", ("DEC_FIRST", "7"): "DEC_HALF_FIRST"}
     if m:
         name = progs[int(m.group(1))]
         return f"{alias.get((name, m.group(2)), name)}/T{m.group(2)}"

@@ -27,8 +27,9 @@ WORK = {
 }
 # the bench step's kernels under the program names bench.py's profile uses
 # (the half decode runs DEC_FIRST at T = 7 and ENC_MID at T = 8)
-BENCH_NAMES = {"ENC_FIRST/T7": ["ENC_FIRST"], "ENC_MID+DEC_HALF_MID/T8": ["ENC_MID", "DEC_HALF_MID"],
-               "ENC_LAST/T7": ["ENC_LAST"], "DEC_HALF_FIRST/T7": ["DEC_HALF_FIRST"],
+BENCH_NAMES = {"ENC_FIRST+DEC_HALF_FIRST/T7": ["ENC_FIRST", "DEC_HALF_FIRST"],
+               "ENC_MID+DEC_HALF_MID/T8": ["ENC_MID", "DEC_HALF_MID"],
+               "ENC_LAST+DEC_HALF_LAST/T7": ["ENC_LAST", "DEC_HALF_LAST"], "DEC_HALF_FIRST/T7": ["DEC_HALF_FIRST"],
                "DEC_HALF_LAST/T7": ["DEC_HALF_LAST"], "rs16::eval_fused_kernel": ["EVAL_POLY"]}
 
 

@@ -16,8 +16,10 @@ from rs16.device import PinnedArray  # noqa: E402
 k = m = 32768
 S = 1024
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+pre = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # streams created before the first host call
 GIB = 2.0 ** 30
 eng = rs16.Engine(0)
+extra_streams = [eng.create_stream() for _ in range(pre)]
 o = np.random.default_rng(5).integers(0, 256, (k, S), dtype=np.uint8)
 ho, hr = PinnedArray(eng, nb * k * S), PinnedArray(eng, nb * m * S)
 ho.array.reshape(nb, k * S)[:] = o.reshape(1, -1)
@@ -42,4 +44,5 @@ for rep in range(int(sys.argv[2]) if len(sys.argv) > 2 else 3):
     for i in range(nb):
         rs16.encode_host(k, m, S, ho.ptr + i * k * S, hr.ptr + i * m * S, engine=eng)
     t1 = time.perf_counter() - t
-    print(f"rep {rep}: one-shot encode x {nb}: {nb * (k + m) * S / t1 / GIB:.1f} GiB/s", flush=True)
+    print(f"rep {rep}: one-shot encode x {nb}: {nb * (k + m) * S / t1 / GIB:.1f} GiB/s (pre-created streams: {pre})",
+          flush=True)
