@@ -473,10 +473,14 @@ enum {
     RS16_DIAG_NO_TILE_LAST = 64,   /* ... always as 8-wave items of 32 quad columns */
     RS16_DIAG_FD_LDS = 128,        /* the general decode's in-tile formal derivative always through LDS */
     RS16_DIAG_COL_RADIX4 = 256,    /* column codec: 4 rows per thread everywhere (no radix-2 form) */
-    RS16_DIAG_NO_IDENTITY = 512    /* a decode whose erased rows are exactly one half of the work rows (all
+    RS16_DIAG_NO_IDENTITY = 512,   /* a decode whose erased rows are exactly one half of the work rows (all
                                       originals lost, all recovery received, k = m = 2^j >= 2048): evaluate
                                       the erasure polynomial and multiply anyway (default: every erasure
                                       log is 0, the multipliers are identities and are skipped) */
+    RS16_DIAG_NO_MID_DIRECT = 1024 /* the general decode's middle pass always as the 2^hi-point IFFT /
+                                      derivative / FFT pass, also when the lost originals lie in at most
+                                      4 of its output rows per column (default there: a direct product
+                                      with the pass's matrix) */
 };
 int rs16_engine_set_diagnostics(rs16_engine* eng, int flags);
 

@@ -144,7 +144,8 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
 extern "C" int rs16_engine_set_diagnostics(rs16_engine* e, int flags) {
     const int old = e->diag;
     e->diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN |
-                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4 | DIAG_NO_IDENTITY);
+                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4 | DIAG_NO_IDENTITY |
+                      DIAG_NO_MID_DIRECT);
     return old;
 }
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
@@ -152,7 +153,8 @@ extern "C" const char* rs16_prog_name(int prog) {
     static const char* names[] = {"GEN_FFT",   "GEN_IFFT",   "ENC_FIRST",     "ENC_MID",
                                   "ENC_LAST",  "ENC_SINGLE", "DEC_FIRST",     "DEC_MID",
                                   "DEC_LAST",  "DEC_SINGLE", "DEC_HALF_LAST", "DEC_HALF_SINGLE",
-                                  "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY", "COL_ENC", "COL_DEC"};
+                                  "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY", "COL_ENC", "COL_DEC",
+                                  "DEC_MID_DIRECT"};
     static_assert(sizeof names / sizeof names[0] == NUM_PROF, "profiling names");
     return (prog >= 0 && prog < NUM_PROF) ? names[prog] : "?";
 }
@@ -267,6 +269,7 @@ extern "C" void rs16_engine_free(rs16_engine* e) {
     e->ws_z.release();
     e->ws_u.release();
     e->ws_fd.release();
+    for (auto& b : e->mid_tab) b.release();
     e->ev_main.release();
     for (auto& l : e->ev_lane) l.release();
     e->ws_flags.release();
@@ -969,8 +972,18 @@ extern "C" int rs16_encode_device_batch(rs16_engine* e, size_t k, size_t m, size
 // Host-resident one-shot codec: shards start and end in host memory.
 // ---------------------------------------------------------------------------
 int rs16_engine::host_slots(rs16_error* err) {
-    for (auto& sl : hslot)
+    for (auto& sl : hslot) {
+#ifdef RS16_EXP_LANE_CUMASK
+        if (!sl.s) {
+            int ncu = 0;
+            RS16_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+            std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
+            RS16_HIP(hipExtStreamCreateWithCUMask(&sl.s, (uint32_t)mask.size(), mask.data()));
+        }
+#else
         if (!sl.s) RS16_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+#endif
+    }
     if (!hev) RS16_HIP(hipEventCreateWithFlags(&hev, hipEventDisableTiming));
     if (int rc = order(stream, err)) return rc;
     // start after the caller's earlier work on the engine stream

@@ -567,6 +567,25 @@ bool rs16_engine::identity_logs(const DecodeGeom& g, uint32_t vary) const {
     return g.high ? g.a_recv == g.a_count : g.b_recv == g.b_count;
 }
 
+int rs16_engine::mid_tables(int L, const uint32_t** out, rs16_error* err) {
+    DevBuf& b = mid_tab[L];
+    if (!b.p) {
+        const HostTables& t = host_tables();
+        const std::vector<uint32_t> ent = mid_matrix_entries(t, L);
+        std::vector<uint32_t> tabs(ent.size() * 20);
+        for (size_t i = 0; i < ent.size(); i++)
+            std::copy_n(&t.mul_tab[(size_t)ent[i] * TAB_DWORDS], 20, &tabs[i * 20]);
+        hipError_t he = b.reserve(tabs.size() * 4);
+        if (he == hipSuccess) he = hipMemcpy(b.p, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice);
+        if (he != hipSuccess) {
+            b.release();
+            return hip_fail(err, he);
+        }
+    }
+    *out = (const uint32_t*)b.p;
+    return RS16_OK;
+}
+
 // The pass sequence of a decode, given what decode_eval left in evset->elog /
 // evset->work32 (erasure logs), evset->rbits (received rows) and evset->zflag (zero tiles).
 int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, const uint8_t* seg_a, const uint8_t* flags_a,
@@ -767,7 +786,24 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.out = U;
     a.need_lo = t0;
     a.need_hi = t1;
+    const size_t lost = g.high ? (size_t)g.b_count - g.b_recv : (size_t)g.a_count - g.a_recv;
+    // Few lost originals: the middle pass's consumed rows may be few enough
+    // for the direct product (mid_direct_kernel; DEC_MID then returns for
+    // the stripes it covered -- decided on the device from lostrange)
+    if (!(diag & DIAG_NO_MID_DIRECT) && lost <= ((size_t)MID_DIRECT_MAX << lo)) {
+        const uint32_t* mt = nullptr;
+        if (int rc = mid_tables(L, &mt, err)) return rc;
+        batch(1u << lo, zs, 0, zs);  // (stripe displacements of the launch)
+        hipEvent_t pev;
+        if (int rc = prof_begin(s, &pev, err)) return rc;
+        if (stamp_buf && stamp_prof == PROF_DEC_MID_DIRECT) a.stamps = (uint64_t*)stamp_buf;
+        RS16_HIP(launch_mid_direct(a, mt, (uint32_t)hi, ns, s));
+        a.stamps = nullptr;
+        if (int rc = prof_end(PROF_DEC_MID_DIRECT, s, pev, err)) return rc;
+        a.mid_direct = MID_DIRECT_MAX;
+    }
     RS16_PASS(DEC_MID, hi, a, batch(1u << lo, zs, 0, zs), s);
+    a.mid_direct = 0;
     a.need_lo = a.need_hi = 0;
     a.lo = 0;
     a.in = Z;
@@ -777,7 +813,6 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     // Few lost originals (lost-range pruning leaves a handful of tiles to
     // this pass): one wave per quad column of each tile (tile_last_kernel)
     // instead of one 8-wave item per 32 quads, whose latency was the pass.
-    const size_t lost = g.high ? (size_t)g.b_count - g.b_recv : (size_t)g.a_count - g.a_recv;
     const bool tile_last = lo == 8 && !(diag & DIAG_NO_TILE_LAST) && (lost <= 2048 || (diag & DIAG_TILE_LAST));
     if (tile_last) {
         const uint32_t tiles = batch(t1 - t0, zs, zs, 0);

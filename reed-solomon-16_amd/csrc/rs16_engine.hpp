@@ -82,6 +82,9 @@ struct rs16_engine {
     uint8_t* d_zero_sink = nullptr;  // zero page (PassArgs::zero, ColArgs::zero)
     // scratch
     rs16::DevBuf ws_z, ws_u, ws_fd, ws_flags;
+    // the general decode's middle pass as v_perm tables of its matrix, per
+    // transform size L (mid_tables; built on first use)
+    rs16::DevBuf mid_tab[17];
     // The decode's eval_poly outputs / pass metadata (written by decode_eval,
     // read by decode_passes).  `evset` points at the set the next decode uses:
     // ev_main, or one of the pipelined host path's per-lane sets (so that
@@ -237,6 +240,9 @@ struct rs16_engine {
     // Every erasure log of the decode is 0 (a whole-half erasure, DESIGN.md
     // 3.13): the multipliers are identities and eval_poly is not launched.
     bool identity_logs(const rs16::DecodeGeom& g, uint32_t vary) const;
+    // Device tables of the L-bit general decode's middle-pass matrix
+    // (mid_matrix_entries), uploaded on first use.
+    int mid_tables(int L, const uint32_t** out, rs16_error* err);
     int decode_eval(const rs16::DecodeGeom& g, const uint8_t* flags_a, const uint8_t* flags_b, hipStream_t s,
                     rs16_error* err, size_t S = 0, size_t nstripes = 1, uint32_t vary = 0, size_t bs_fa = 0,
                     size_t bs_fb = 0);

@@ -32,6 +32,10 @@ struct HostTables {
     // sum_{j < n} W[j] mod 65535 (sum over all rows of W = 65536 LogWalsh[0])
     std::vector<uint32_t> col_k;
 };
+// DEC_MID of an L-bit general decode as a 2^hi x 2^hi matrix of mul-table
+// entries (rs16_tables.cpp; the direct middle pass, rs16_engine::mid_matrix)
+std::vector<uint32_t> mid_matrix_entries(const HostTables& t, int L);
+
 constexpr uint32_t COL_LMIN = 6, COL_LMAX = 10;
 // (and the general decoder's 2^11-row transform, skew delta 0 only)
 constexpr uint32_t COL_LGEN = 11;
@@ -86,6 +90,7 @@ enum ProfId : int {
     PROF_EVAL_POLY,
     PROF_COL_ENC,  // one-launch codec (rs16_col.hip): encode
     PROF_COL_DEC,  // one-launch codec: half-transform decode
+    PROF_DEC_MID_DIRECT,  // the general decode's middle pass as a direct product (mid_direct_kernel)
     NUM_PROF
 };
 
@@ -189,6 +194,10 @@ struct PassArgs {
     uint32_t* rcount;
     const uint8_t* cnt_flags;
     uint32_t cnt_base, cnt_seg;
+    // DEC_MID: mid_direct_kernel runs before it and produces U itself when
+    // the consumed tile rows (from lostrange) are at most mid_direct; those
+    // DEC_MID workgroups return at once (0: no direct kernel)
+    uint32_t mid_direct;
 };
 
 // One-launch codec for 2^9 / 2^10-row transforms (rs16_col.hip): one
@@ -276,6 +285,7 @@ enum DiagFlags : int {
     DIAG_FD_LDS = 128,        // DEC_MID's in-tile formal derivative always through the LDS image (tile_fd)
     DIAG_COL_RADIX4 = 256,    // column codec: the 4-rows-per-thread form for every transform (col_kernel)
     DIAG_NO_IDENTITY = 512,   // whole-half erasures: eval_poly and the per-row multipliers anyway (identity_logs)
+    DIAG_NO_MID_DIRECT = 1024, // the general decode's middle pass always as DEC_MID (no mid_direct_kernel)
 };
 
 constexpr size_t RS16_ZERO_BYTES = 65536;
@@ -286,6 +296,14 @@ hipError_t launch_pass(int prog, int T, const PassArgs& a, uint32_t num_tiles, h
 // tile_last_kernel): `num_tiles` tiles (x stripes, PassArgs::stripe_tiles)
 // from a.tile_base, rows at lo = 0.
 hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s);
+// The general decode's middle pass as a direct product (rs16_pass.hip
+// mid_direct_kernel): U rows [need_lo, need_hi) of every tile column j from
+// the live Z rows and mtab (rs16_engine::mid_tables: 2^hi x 2^hi v_perm
+// tables of mid_matrix_entries, 80 bytes each, row-major), for `ns`
+// stripes; a stripe whose consumed rows exceed MID_DIRECT_MAX does nothing
+// (DEC_MID computes it).
+constexpr uint32_t MID_DIRECT_MAX = 4;
+hipError_t launch_mid_direct(const PassArgs& a, const uint32_t* mtab, uint32_t hi, uint32_t ns, hipStream_t s);
 
 // Elementwise / small kernels.
 hipError_t launch_mul(uint8_t* x, size_t bytes, uint32_t entry, const uint32_t* mul_tab, hipStream_t s);

@@ -206,6 +206,16 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
     return ur < lim && lr < lim - ur;
 }
 
+// The consumed U rows [nlo, nhi) of the general decode's middle pass, when
+// at most MID_DIRECT_MAX (mid_direct_kernel: the direct product).
+__device__ __forceinline__ bool mid_need(const PassArgs& a, uint32_t& nlo, uint32_t& nhi) {
+    const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
+    if (r0 >= r1) return false;
+    nlo = max(a.need_lo, r0 >> a.lo);
+    nhi = min(a.need_hi, ((r1 - 1) >> a.lo) + 1);
+    return nhi > nlo && nhi - nlo <= MID_DIRECT_MAX;
+}
+
 // Priority schedule: a wave lowers its issue priority (s_setprio 3 -> 0) as
 // its item progresses, so that waves that are behind win the arbitration.
 // Hardware age order alone lets the oldest workgroup of a CU run ahead and
@@ -1436,6 +1446,11 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
         // before its table staging and row loads, so its slot frees at once
         if (a.zflags && ((((cu32p)a.zflags)[tile >> 2] >> (8 * (tile & 3))) & 1u)) return;
     }
+    if constexpr (P == DEC_MID) {
+        // mid_direct_kernel computed this stripe's consumed rows already
+        uint32_t nlo, nhi;
+        if (a.mid_direct && a.lostrange && mid_need(a, nlo, nhi)) return;
+    }
     if constexpr (P == DEC_LAST) {
         // A tile without a lost original stores nothing: return before any
         // load (the decode's lost rows are [lostrange[0], lostrange[1])).
@@ -1672,6 +1687,130 @@ hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s
     if (num_tiles == 0 || a.qrow == 0) return hipSuccess;
     const uint32_t nwg = num_tiles * ((a.qrow + 3) / 4);
     hipLaunchKernelGGL(tile_last_kernel, dim3(nwg), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The general decode's middle pass as a direct product.  DEC_MID is the same
+// linear map u = FFT_hi (I + H) IFFT_hi z on every tile column j (rows
+// t << lo | j; its twiddles do not involve j), a 2^hi x 2^hi matrix M over
+// GF(2^16) (mid_matrix_entries, rs16_tables.cpp).  When the lost originals
+// lie in few last-pass tiles, DEC_LAST consumes only the U rows t in
+// [nlo, nhi) -- nhi - nlo <= MID_DIRECT_MAX -- and each is a sum over the
+// live z rows (DEC_FIRST tiles with a received row, zflags):
+//   u[o << lo | j] = sum over live t of M[o][t] z[t << lo | j]
+// -- (nhi - nlo) x (live rows) multiplies per column instead of DEC_MID's
+// 2^hi-point IFFT, derivative and output-pruned FFT (at the reference
+// bench's 1 % loss: 2 x 129 against ~1300 butterflies, and one dispatch
+// round instead of two).  Workgroup = (column j, 64-quad slab, stripe);
+// its 8 waves take the rows t = w mod 8 (the zero tiles cluster, so
+// interleaved), all of a wave's rows requested at once, and multiply them by
+// the tables of rows [nlo, nhi) of M in LDS (one LDS-DMA copy of the
+// contiguous v_perm tables), then XOR their partial sums through LDS; wave o
+// stores row nlo + o.  A stripe whose consumed rows exceed
+// MID_DIRECT_MAX returns here and DEC_MID computes it (PassArgs::mid_direct).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(512) mid_direct_kernel(PassArgs a, const uint32_t* mtab, uint32_t hi) {
+    constexpr uint32_t W = 8, RPW = 256 / W;  // waves; rows per wave at 2^hi = 256
+    extern __shared__ __attribute__((aligned(16))) uint8_t mlds[];
+    const uint32_t j = blockIdx.x, t0 = threadIdx.x, lane = t0 & 63, w = uni(t0 >> 6);
+    if (blockIdx.z) {  // stripe z (PassArgs::stripe_tiles convention: displacements per stripe)
+        const uint32_t st = blockIdx.z;
+        a.in += st * a.bs_in;
+        a.out += st * a.bs_out;
+        if (a.zflags) a.zflags += st * a.bs_zflags;
+        a.lostrange += st * a.bs_lost;
+    }
+    uint32_t nlo, nhi;
+    if (!mid_need(a, nlo, nhi)) return;
+    const uint32_t N = 1u << hi, nout = nhi - nlo, rpw = N / W;
+    RS16_STAMP(a, 0);
+    const uint32_t Qg = blockIdx.y * 64 + lane;
+    const bool active = Qg < a.qrow;
+    const uint32_t offL = (Qg >> 3) * 64 + (Qg & 7) * 4;
+    const uint8_t* zpage = a.zero + (offL & 0x7FFFu);
+    // every row of the wave (t = w + 8 u) requested at once -- one round trip
+    // per wave; a dead row (DEC_FIRST tile without a received row) reads the
+    // zero page -- then the tables of rows [nlo, nhi) of M by LDS-DMA
+    // (lane u reads row u's zero-tile flag: one load and a ballot)
+    const bool lv_lane = lane < rpw && !(a.zflags && a.zflags[w + W * lane]);
+    const uint64_t live = __ballot(lv_lane);
+    const uint8_t* rbase = a.in + ((uint64_t)w << a.lo | j) * a.S_in;
+    const uint64_t rstride = ((uint64_t)W << a.lo) * a.S_in;
+    uint32_t zl[RPW], zh[RPW];
+#pragma unroll
+    for (uint32_t u = 0; u < RPW; u++) {
+        const bool lv = (live >> u) & 1u;
+        const uint32_t* p = (const uint32_t*)(active && lv ? rbase + u * rstride + offL : zpage);
+        zl[u] = p[0];
+        zh[u] = p[8];
+    }
+    uint4* tabs = (uint4*)mlds;
+    colops::dma_copy<W * 64>((const uint8_t*)(mtab + (size_t)nlo * N * 20), mlds, nout * N * 80);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();  // tables in LDS
+    RS16_STAMP(a, 1);
+    uint32_t acc[MID_DIRECT_MAX][2] = {};
+#ifdef RS16_EXP_MD_NOLDS
+    uint32_t tx[2][20];
+    load_table_lds(tx[0], tabs);
+    load_table_lds(tx[1], tabs + 5);
+#endif
+#pragma unroll
+    for (uint32_t u = 0; u < RPW; u++) {
+        if (!((live >> u) & 1u)) continue;  // (uniform)
+        const uint32_t t = w + W * u;
+#pragma unroll
+        for (uint32_t o = 0; o < MID_DIRECT_MAX; o++) {
+            if (o >= nout) break;
+#ifdef RS16_EXP_MD_NOLDS
+            mul_xor(acc[o][0], acc[o][1], zl[u], zh[u], tx[o & 1]);
+            (void)t;
+#else
+            uint32_t tt[20];
+            load_table_lds(tt, tabs + (o * N + t) * 5);
+            mul_xor(acc[o][0], acc[o][1], zl[u], zh[u], tt);
+#endif
+        }
+    }
+    RS16_STAMP(a, 2);
+    // XOR the waves' partial sums: row o by wave o
+    __syncthreads();  // (the tables are no longer read: the partials reuse their LDS)
+    uint2* part = (uint2*)mlds;
+#pragma unroll
+    for (uint32_t o = 0; o < MID_DIRECT_MAX; o++)
+        if (o < nout) part[(w * MID_DIRECT_MAX + o) * 64 + lane] = make_uint2(acc[o][0], acc[o][1]);
+    __syncthreads();
+    if (w < nout) {
+        uint32_t xl = 0, xh = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < W; v++) {
+            const uint2 q = part[(v * MID_DIRECT_MAX + w) * 64 + lane];
+            xl ^= q.x;
+            xh ^= q.y;
+        }
+        if (active) {
+            uint32_t* p = (uint32_t*)(a.out + ((uint64_t)(nlo + w) << a.lo | j) * a.S_out + offL);
+            p[0] = xl;
+            p[8] = xh;
+        }
+    }
+    RS16_STAMP_END(a);
+}
+
+hipError_t launch_mid_direct(const PassArgs& a, const uint32_t* mtab, uint32_t hi, uint32_t ns, hipStream_t s) {
+    if (a.qrow == 0 || ns == 0) return hipSuccess;
+    const uint32_t N = 1u << hi;
+    // tables of up to MID_DIRECT_MAX rows (bounded by the host's consumed range)
+    const uint32_t rows = std::min(MID_DIRECT_MAX, a.need_hi > a.need_lo ? a.need_hi - a.need_lo : 0u);
+    if (rows == 0 || hi > 8 || hi < 3) return rows == 0 ? hipSuccess : hipErrorInvalidValue;
+    const size_t lds = std::max((size_t)rows * N * 80, (size_t)8 * MID_DIRECT_MAX * 64 * 8);
+    if (lds > 65536) {  // (as launch_pass: set on every call, i.e. on the current device)
+        hipError_t e = hipFuncSetAttribute((const void*)mid_direct_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(mid_direct_kernel, dim3(1u << a.lo, (a.qrow + 63) / 64, ns), dim3(512), lds, s, a, mtab, hi);
     return hipGetLastError();
 }
 

@@ -188,6 +188,60 @@ void build(HostTables& t) {
 }
 }  // namespace
 
+// The general decode's middle pass as a matrix (rs16_engine::mid_matrix):
+// DEC_MID maps the 2^hi rows t << lo | j of every tile column j (lo = L / 2,
+// hi = L - lo, skew 0) by u = FFT_hi (I + H) IFFT_hi z -- the IFFT / FFT
+// layers lo .. L-1 (src/engine/engine_nosimd.rs fft / ifft: twiddle
+// skew[r + dist - 1] of the block at global row r, butterflies x ^= y m, y ^= x
+// and y ^= x, x ^= y m) around the high-bit half of the formal derivative
+// (src/engine.rs formal_derivative: row t takes row t | 2^c for every tile
+// bit c clear in t).  The twiddle indices do not involve j, so one 2^hi x
+// 2^hi matrix serves every column; entry [o][t] = the log of M[o][t]
+// (ZERO_ENTRY for 0), column t computed as the image of the unit vector at t.
+std::vector<uint32_t> mid_matrix_entries(const HostTables& t, int L) {
+    const int lo = L / 2, hi = L - lo;
+    const uint32_t N = 1u << hi;
+    const uint16_t one = t.exp[0];  // the element whose log is 0
+    std::vector<uint32_t> ent((size_t)N * N, ZERO_ENTRY);
+    std::vector<uint16_t> v(N), w(N);
+    auto tw = [&](uint32_t r_tile, int kb) {  // twiddle log of the block at tile row r_tile, layer kb
+        const uint32_t m = (uint32_t)(lo + kb);
+        return (uint32_t)t.skew[((size_t)r_tile << lo) + (1u << m) - 1];
+    };
+    for (uint32_t c = 0; c < N; c++) {
+        std::fill(v.begin(), v.end(), 0);
+        v[c] = one;
+        for (int kb = 0; kb < hi; kb++) {  // IFFT, low layers first
+            const uint32_t d = 1u << kb;
+            for (uint32_t r = 0; r < N; r += 2 * d) {
+                const uint32_t lm = tw(r, kb);
+                for (uint32_t i = r; i < r + d; i++) {
+                    v[i + d] ^= v[i];
+                    if (lm != GF_MODULUS) v[i] ^= gf_mul(t, v[i + d], lm);
+                }
+            }
+        }
+        for (uint32_t i = 0; i < N; i++) {  // (I + H): the formal derivative's tile bits
+            uint16_t x = v[i];
+            for (uint32_t b = 1; b < N; b <<= 1)
+                if (!(i & b)) x ^= v[i | b];
+            w[i] = x;
+        }
+        for (int kb = hi - 1; kb >= 0; kb--) {  // FFT, high layers first
+            const uint32_t d = 1u << kb;
+            for (uint32_t r = 0; r < N; r += 2 * d) {
+                const uint32_t lm = tw(r, kb);
+                for (uint32_t i = r; i < r + d; i++) {
+                    if (lm != GF_MODULUS) w[i] ^= gf_mul(t, w[i + d], lm);
+                    w[i + d] ^= w[i];
+                }
+            }
+        }
+        for (uint32_t o = 0; o < N; o++) ent[(size_t)o * N + c] = w[o] ? t.log[w[o]] : ZERO_ENTRY;
+    }
+    return ent;
+}
+
 const HostTables& host_tables() {
     std::call_once(g_once, [] { build(g_tables); });
     return g_tables;

@@ -29,7 +29,7 @@ __all__ = [
     "supports", "validate", "use_high_rate", "encode_device_batch", "decode_device_batch", "encoder_work_count", "decoder_work_count",
     "RATE_DEFAULT", "RATE_HIGH", "RATE_LOW", "GF_ORDER", "GF_MODULUS", "set_diagnostics",
     "DIAG_FORCE_VOFF64", "DIAG_EVAL_TWO_KERNEL", "DIAG_EVAL_FULL", "DIAG_NO_COLUMN", "DIAG_FORCE_COLUMN",
-    "DIAG_TILE_LAST", "DIAG_NO_TILE_LAST", "DIAG_FD_LDS", "DIAG_COL_RADIX4", "DIAG_NO_IDENTITY", "encode_host", "decode_host",
+    "DIAG_TILE_LAST", "DIAG_NO_TILE_LAST", "DIAG_FD_LDS", "DIAG_COL_RADIX4", "DIAG_NO_IDENTITY", "DIAG_NO_MID_DIRECT", "encode_host", "decode_host",
     "encode_host_batch", "decode_host_batch", "decode_prepare", "decode_device_prepared",
     "encode_host_multi", "decode_host_multi", "Comm", "column_slice", "scatter_columns", "gather_columns",
 ]
@@ -39,6 +39,7 @@ GF_MODULUS = 65535
 # rs16_engine_set_diagnostics flags (include/rs16.h): alternative code paths for tests
 DIAG_FORCE_VOFF64, DIAG_EVAL_TWO_KERNEL, DIAG_EVAL_FULL, DIAG_NO_COLUMN, DIAG_FORCE_COLUMN = 1, 2, 4, 8, 16
 DIAG_TILE_LAST, DIAG_NO_TILE_LAST, DIAG_FD_LDS, DIAG_COL_RADIX4, DIAG_NO_IDENTITY = 32, 64, 128, 256, 512
+DIAG_NO_MID_DIRECT = 1024
 # Test convenience only: the flags set_diagnostics() without an engine gave
 # every live engine, and that engines created later in this Python process
 # start with.  The library itself keeps the switches per engine.

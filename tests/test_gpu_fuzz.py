@@ -35,7 +35,7 @@ pytestmark = pytest.mark.gpu
 GF_ORDER = 65536
 DIAGS = (rs16.DIAG_FORCE_VOFF64, rs16.DIAG_EVAL_TWO_KERNEL, rs16.DIAG_EVAL_FULL, rs16.DIAG_NO_COLUMN,
          rs16.DIAG_FORCE_COLUMN, rs16.DIAG_TILE_LAST, rs16.DIAG_NO_TILE_LAST, rs16.DIAG_FD_LDS,
-         rs16.DIAG_COL_RADIX4, rs16.DIAG_NO_IDENTITY)
+         rs16.DIAG_COL_RADIX4, rs16.DIAG_NO_IDENTITY, rs16.DIAG_NO_MID_DIRECT)
 BUDGET = 3 << 20  # bytes of originals + recovery per case (all stripes)
 
 
