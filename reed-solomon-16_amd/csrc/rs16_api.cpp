@@ -972,18 +972,8 @@ extern "C" int rs16_encode_device_batch(rs16_engine* e, size_t k, size_t m, size
 // Host-resident one-shot codec: shards start and end in host memory.
 // ---------------------------------------------------------------------------
 int rs16_engine::host_slots(rs16_error* err) {
-    for (auto& sl : hslot) {
-#ifdef RS16_EXP_LANE_CUMASK
-        if (!sl.s) {
-            int ncu = 0;
-            RS16_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-            std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
-            RS16_HIP(hipExtStreamCreateWithCUMask(&sl.s, (uint32_t)mask.size(), mask.data()));
-        }
-#else
+    for (auto& sl : hslot)
         if (!sl.s) RS16_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
-#endif
-    }
     if (!hev) RS16_HIP(hipEventCreateWithFlags(&hev, hipEventDisableTiming));
     if (int rc = order(stream, err)) return rc;
     // start after the caller's earlier work on the engine stream

@@ -1713,7 +1713,10 @@ hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s
 __global__ void __launch_bounds__(512) mid_direct_kernel(PassArgs a, const uint32_t* mtab, uint32_t hi) {
     constexpr uint32_t W = 8, RPW = 256 / W;  // waves; rows per wave at 2^hi = 256
     extern __shared__ __attribute__((aligned(16))) uint8_t mlds[];
-    const uint32_t j = blockIdx.x, t0 = threadIdx.x, lane = t0 & 63, w = uni(t0 >> 6);
+    // blockIdx.x = column j x slabs + 64-quad slab (one index: the stamps' workgroup id)
+    const uint32_t nslab = (a.qrow + 63) / 64;
+    const uint32_t j = blockIdx.x / nslab, slab = blockIdx.x - j * nslab;
+    const uint32_t t0 = threadIdx.x, lane = t0 & 63, w = uni(t0 >> 6);
     if (blockIdx.z) {  // stripe z (PassArgs::stripe_tiles convention: displacements per stripe)
         const uint32_t st = blockIdx.z;
         a.in += st * a.bs_in;
@@ -1725,53 +1728,62 @@ __global__ void __launch_bounds__(512) mid_direct_kernel(PassArgs a, const uint3
     if (!mid_need(a, nlo, nhi)) return;
     const uint32_t N = 1u << hi, nout = nhi - nlo, rpw = N / W;
     RS16_STAMP(a, 0);
-    const uint32_t Qg = blockIdx.y * 64 + lane;
+    const uint32_t Qg = slab * 64 + lane;
     const bool active = Qg < a.qrow;
     const uint32_t offL = (Qg >> 3) * 64 + (Qg & 7) * 4;
     const uint8_t* zpage = a.zero + (offL & 0x7FFFu);
-    // every row of the wave (t = w + 8 u) requested at once -- one round trip
-    // per wave; a dead row (DEC_FIRST tile without a received row) reads the
-    // zero page -- then the tables of rows [nlo, nhi) of M by LDS-DMA
+    // The wave's rows t = w + 8 u (a dead row -- DEC_FIRST tile without a
+    // received row -- reads the zero page) and the tables of rows [nlo, nhi)
+    // of M (LDS-DMA, L2-resident after the first workgroups).
     // (lane u reads row u's zero-tile flag: one load and a ballot)
     const bool lv_lane = lane < rpw && !(a.zflags && a.zflags[w + W * lane]);
     const uint64_t live = __ballot(lv_lane);
     const uint8_t* rbase = a.in + ((uint64_t)w << a.lo | j) * a.S_in;
     const uint64_t rstride = ((uint64_t)W << a.lo) * a.S_in;
-    uint32_t zl[RPW], zh[RPW];
+    // Rows in batches of RPB: batch b + 1 is requested once batch b has
+    // landed, before batch b's multiplies.  (All rows requested at once land
+    // together at the end of the chip-wide load phase and the VALU idles
+    // through it: 14.8 us per workgroup, half of it loads,
+    // `profiles/r05_mid_direct.txt`.)
+    constexpr uint32_t RPB = 8, NB = RPW / RPB;
+    uint32_t zl[2][RPB], zh[2][RPB];
+    auto fetch = [&](uint32_t b, uint32_t (&l)[RPB], uint32_t (&h)[RPB]) {
 #pragma unroll
-    for (uint32_t u = 0; u < RPW; u++) {
-        const bool lv = (live >> u) & 1u;
-        const uint32_t* p = (const uint32_t*)(active && lv ? rbase + u * rstride + offL : zpage);
-        zl[u] = p[0];
-        zh[u] = p[8];
-    }
+        for (uint32_t v = 0; v < RPB; v++) {
+            const uint32_t u = b * RPB + v;
+            const uint32_t* p = (const uint32_t*)(active && ((live >> u) & 1u) ? rbase + u * rstride + offL : zpage);
+            l[v] = p[0];
+            h[v] = p[8];
+        }
+    };
+    fetch(0, zl[0], zh[0]);
     uint4* tabs = (uint4*)mlds;
     colops::dma_copy<W * 64>((const uint8_t*)(mtab + (size_t)nlo * N * 20), mlds, nout * N * 80);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();  // tables in LDS
     RS16_STAMP(a, 1);
     uint32_t acc[MID_DIRECT_MAX][2] = {};
-#ifdef RS16_EXP_MD_NOLDS
-    uint32_t tx[2][20];
-    load_table_lds(tx[0], tabs);
-    load_table_lds(tx[1], tabs + 5);
-#endif
+    auto multiply = [&](uint32_t b, const uint32_t (&l)[RPB], const uint32_t (&h)[RPB]) {
 #pragma unroll
-    for (uint32_t u = 0; u < RPW; u++) {
-        if (!((live >> u) & 1u)) continue;  // (uniform)
-        const uint32_t t = w + W * u;
+        for (uint32_t v = 0; v < RPB; v++) {
+            const uint32_t u = b * RPB + v;
+            if (!((live >> u) & 1u)) continue;  // (uniform)
+            const uint32_t t = w + W * u;
 #pragma unroll
-        for (uint32_t o = 0; o < MID_DIRECT_MAX; o++) {
-            if (o >= nout) break;
-#ifdef RS16_EXP_MD_NOLDS
-            mul_xor(acc[o][0], acc[o][1], zl[u], zh[u], tx[o & 1]);
-            (void)t;
-#else
-            uint32_t tt[20];
-            load_table_lds(tt, tabs + (o * N + t) * 5);
-            mul_xor(acc[o][0], acc[o][1], zl[u], zh[u], tt);
-#endif
+            for (uint32_t o = 0; o < MID_DIRECT_MAX; o++) {
+                if (o >= nout) break;
+                uint32_t tt[20];
+                load_table_lds(tt, tabs + (o * N + t) * 5);
+                mul_xor(acc[o][0], acc[o][1], l[v], h[v], tt);
+            }
         }
+    };
+#pragma unroll
+    for (uint32_t b = 0; b < NB; b++) {
+        if (b * RPB >= rpw) break;  // (uniform: 2^hi < 256)
+        if (b + 1 < NB && (b + 1) * RPB < rpw) fetch(b + 1, zl[(b + 1) & 1], zh[(b + 1) & 1]);
+        multiply(b, zl[b & 1], zh[b & 1]);
+        __builtin_amdgcn_s_waitcnt(vmcnt_wait(0));
     }
     RS16_STAMP(a, 2);
     // XOR the waves' partial sums: row o by wave o
@@ -1810,7 +1822,8 @@ hipError_t launch_mid_direct(const PassArgs& a, const uint32_t* mtab, uint32_t h
                                            (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(mid_direct_kernel, dim3(1u << a.lo, (a.qrow + 63) / 64, ns), dim3(512), lds, s, a, mtab, hi);
+    hipLaunchKernelGGL(mid_direct_kernel, dim3((1u << a.lo) * ((a.qrow + 63) / 64), 1, ns), dim3(512), lds, s, a, mtab,
+                       hi);
     return hipGetLastError();
 }
 
