@@ -911,16 +911,17 @@ def main():
         # stripe holds this stripe's data: each recovery must equal the one
         # checked against the oracle fixture above, each decode restore it.
         nb = 8
-        hb_o, hb_r = PinnedArray(eng, nb * k * S), PinnedArray(eng, nb * m * S)
+        heng = eng
+        hb_o, hb_r = PinnedArray(heng, nb * k * S), PinnedArray(heng, nb * m * S)
         hb_o.array.reshape(nb, k * S)[:] = original.reshape(1, -1)
         fob = np.tile(of, nb)
         frb = np.tile(rf, nb)
 
         def batch_encode():
-            rs16.encode_host_batch(k, m, S, nb, hb_o.ptr, k * S, hb_r.ptr, m * S, engine=eng)
+            rs16.encode_host_batch(k, m, S, nb, hb_o.ptr, k * S, hb_r.ptr, m * S, engine=heng)
 
         def batch_decode():
-            rs16.decode_host_batch(k, m, S, nb, hb_o.ptr, k * S, fob, k, hb_r.ptr, m * S, frb, m, engine=eng)
+            rs16.decode_host_batch(k, m, S, nb, hb_o.ptr, k * S, fob, k, hb_r.ptr, m * S, frb, m, engine=heng)
 
         batch_encode()
         assert all(np.array_equal(hb_r.array.reshape(nb, m, S)[i], recovery) for i in range(nb)), \
@@ -943,10 +944,28 @@ def main():
             "decode_gib_s": world * nb * (k + m) * S * n5 / tbd / GIB,
             "encode_ms_per_call": tbe / n5 * 1e3, "decode_ms_per_call": tbd / n5 * 1e3,
             "link_bytes_per_call": {"encode": nb * (k + m) * S, "decode_100pct": nb * (k + loss) * S},
-            "path": "pinned host stripes, two in flight: H2D of stripe i+1 and D2H of stripe i-1 on two copy "
-                    "streams around stripe i's codec (rs16_encode_host_batch / rs16_decode_host_batch); "
+            "path": "pinned host stripes, two in flight: stripe i runs H2D -> codec -> D2H on lane i & 1 (a "
+                    "stream with buffers of its own), the lanes half a period apart so that one lane's D2H "
+                    "meets the other's H2D (rs16_encode_host_batch / rs16_decode_host_batch, DESIGN.md 3.10); "
                     "every stripe's recovery == the fixture-checked one, every decode restored"}
         del hb_o, hb_r
+        # The same calls in a fresh child process (scripts/probe_hostbatch.py,
+        # which checks every restored stripe): in this process, after the
+        # extras above, they run slower, and not for any cause found so far
+        # (NUMA node, streams created before the lanes, an RCCL communicator,
+        # the engine's state, GPU clocks after load: DESIGN.md 6.R5)
+        if world == 1:
+            res = subprocess.run([sys.executable, str(Path(__file__).resolve().parent / "scripts" / "probe_hostbatch.py"),
+                                  str(nb), "4"], capture_output=True, text=True, timeout=300)
+            last = [ln for ln in res.stdout.splitlines() if ln.startswith("rep 3: encode")]
+            if res.returncode == 0 and last and "restored True" in last[0]:
+                ln = last[0]
+                enc = float(ln.split("encode ")[1].split(" GiB/s")[0])
+                dec = float(ln.split("decode ")[1].split(" GiB/s")[0])
+                extra["host_batch_pipelined"]["fresh_process"] = {
+                    "encode_gib_s": enc, "decode_gib_s": dec,
+                    "note": "4th call of each in a child process (scripts/probe_hostbatch.py, 8 stripes, restored "
+                            "checked); the first calls of a process pay buffer setup"}
 
     if not args.no_extra and world == 1:
         # The reference's own API benchmark (ReedSolomonEncoder / Decoder with

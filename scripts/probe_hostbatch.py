@@ -20,6 +20,10 @@ pre = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # streams created before the
 GIB = 2.0 ** 30
 eng = rs16.Engine(0)
 extra_streams = [eng.create_stream() for _ in range(pre)]
+if len(sys.argv) > 4 and sys.argv[4] == "rccl":  # an RCCL communicator created and closed first (as in bench.py)
+    (comm,) = rs16.Comm.init_all([eng])
+    comm.close()
+
 o = np.random.default_rng(5).integers(0, 256, (k, S), dtype=np.uint8)
 ho, hr = PinnedArray(eng, nb * k * S), PinnedArray(eng, nb * m * S)
 ho.array.reshape(nb, k * S)[:] = o.reshape(1, -1)
@@ -28,6 +32,21 @@ fr = np.ones(nb * m, np.uint8)
 hfo, hfr = PinnedArray(eng, nb * k), PinnedArray(eng, nb * m)
 hfo.array[:] = fo
 hfr.array[:] = fr
+if len(sys.argv) > 4 and sys.argv[4] == "oneshot":  # the one-shot host path first (as in bench.py)
+    for _ in range(3):
+        rs16.encode_host(k, m, S, ho.ptr, hr.ptr, engine=eng)
+if len(sys.argv) > 4 and sys.argv[4].startswith("hot"):  # seconds of device-resident steps right before
+    from rs16.device import DeviceArray
+    d_o, d_r = DeviceArray.from_numpy(eng, o), DeviceArray(eng, m * S)
+    f0 = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+    f1 = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+    d_x = DeviceArray(eng, k * S)
+    t_end = time.perf_counter() + float(sys.argv[4][3:] or 1)
+    while time.perf_counter() < t_end:
+        for _ in range(50):
+            rs16.encode_device(k, m, S, d_o.ptr, d_r.ptr, engine=eng)
+            rs16.decode_device(k, m, S, d_x.ptr, f0.ptr, d_r.ptr, f1.ptr, 0, m, engine=eng)
+        eng.synchronize()
 for rep in range(int(sys.argv[2]) if len(sys.argv) > 2 else 3):
     t = time.perf_counter()
     rs16.encode_host_batch(k, m, S, nb, ho.ptr, k * S, hr.ptr, m * S, engine=eng)
