@@ -232,7 +232,9 @@ def sustained(eng, step, step_bytes, dist, seconds=0.45):
 
     import numpy as np
 
-    hip = C.CDLL("libamdhip64.so")
+    from rs16._lib import hip_runtime
+
+    hip = hip_runtime()  # (librs16's HIP runtime, not the copy torch brings along at N > 1)
     hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
     hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
     hip.hipEventSynchronize.argtypes = [C.c_void_p]

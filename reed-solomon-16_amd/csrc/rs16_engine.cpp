@@ -790,7 +790,8 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     // Few lost originals: the middle pass's consumed rows may be few enough
     // for the direct product (mid_direct_kernel; DEC_MID then returns for
     // the stripes it covered -- decided on the device from lostrange)
-    if (!(diag & DIAG_NO_MID_DIRECT) && lost <= ((size_t)MID_DIRECT_MAX << lo)) {
+    // (grid z = the stripe: at most 65535 of them in one launch)
+    if (!(diag & DIAG_NO_MID_DIRECT) && lost <= ((size_t)MID_DIRECT_MAX << lo) && ns <= 65535) {
         const uint32_t* mt = nullptr;
         if (int rc = mid_tables(L, &mt, err)) return rc;
         batch(1u << lo, zs, 0, zs);  // (stripe displacements of the launch)

@@ -130,3 +130,19 @@ def lib():
             f.restype, f.argtypes = res, args
         _lib = L
     return _lib
+
+
+def hip_runtime():
+    """The HIP runtime librs16.so runs on, for the few direct HIP calls of the
+    diagnostics (events in bench.py).  A process that imported torch holds a
+    second libamdhip64 (torch's bundled copy, soname libamdhip64.so): loading
+    "libamdhip64.so" by name resolves to that one, which does not share
+    librs16's device context (hipGetDevice there fails with 100).  This
+    returns the mapped copy that is not torch's."""
+    lib()
+    with open("/proc/self/maps") as maps:
+        for line in maps:
+            path = line.split()[-1] if "/" in line else ""
+            if "libamdhip64" in path and "/torch/" not in path:
+                return C.CDLL(path)
+    return C.CDLL("libamdhip64.so")

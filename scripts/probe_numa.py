@@ -31,7 +31,8 @@ def main():
         nodes[int(d.name[4:])] = cpulist((d / "cpulist").read_text())
     allowed = sorted(os.sched_getaffinity(0))
     print("nodes:", {n: (len(c), c[0], c[-1]) for n, c in nodes.items()}, "allowed:", len(allowed), allowed[:4], "...")
-    hip = C.CDLL("libamdhip64.so")
+    from rs16._lib import hip_runtime  # noqa: E402
+    hip = hip_runtime()
     bus = C.create_string_buffer(64)
     hip.hipDeviceGetPCIBusId(bus, 64, 0)
     bdf = bus.value.decode().lower()

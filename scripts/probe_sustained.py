@@ -18,7 +18,8 @@ import rs16  # noqa: E402
 from rs16.device import DeviceArray  # noqa: E402
 from rs16.util import generate_original  # noqa: E402
 
-hip = C.CDLL("libamdhip64.so")
+from rs16._lib import hip_runtime  # noqa: E402
+hip = hip_runtime()
 hip.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
 hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
 hip.hipEventSynchronize.argtypes = [C.c_void_p]
