@@ -64,6 +64,11 @@ namespace rs16 {
 
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
 
+// (timing A/B builds: -DRS16_NO_EARLY_B=1 keeps the IFFT-only passes' stores after the last block)
+#ifndef RS16_NO_EARLY_B
+#define RS16_NO_EARLY_B 0
+#endif
+
 enum LoadMode { LD_PLAIN = 0, LD_GATHER_ENC, LD_GATHER_DEC, LD_DEC_LAST };
 enum StoreMode { ST_PLAIN = 0, ST_RECOVERY, ST_RESTORE };
 
@@ -1198,6 +1203,84 @@ template <int P, int T> struct EarlyStore {
     }
 };
 
+// The same for a pass that ends with its IFFT in layout B (ENC_FIRST, the
+// decoders' first pass, GEN_IFFT): the rows with register bit 0 clear and
+// those with it set go through the block's layers separately -- the layer of
+// register bit 0 (layout-B bit SHB, the first one at T = 8) all in the first
+// half, every higher layer's butterfly pairs m, m + 2^rb with m of the half's
+// parity -- so the even rows are final after the first half and are stored
+// there (fin), and the odd rows' butterflies run while those stores drain.
+// Same groups, tables and butterflies as layers<.., LB = true, .., IFFT>,
+// in another order; every group's table is read (LDS) one group ahead.
+template <int T> struct HalfSeq {
+    static constexpr int SH = Geo<T>::SHB, NR = Geo<T>::NR;
+    // step g -> half * 256 + kb * 16 + gi
+    static constexpr int at(int g) {
+        int n = 0;
+        for (int half = 0; half < 2; half++)
+            for (int kb = Geo<T>::R; kb < T; kb++) {
+                const int rb = kb - SH;
+                if (rb == 0 && half == 1) continue;  // (bit 0's layer: all in the first half)
+                for (int gi = 0; gi < (NR >> (rb + 1)); gi++)
+                    if (n++ == g) return half * 256 + kb * 16 + gi;
+            }
+        return -1;
+    }
+    static constexpr int total() {
+        int g = 0;
+        while (at(g) >= 0) g++;
+        return g;
+    }
+};
+template <int T, int G, class FIN> struct HalfLoop {
+    static __device__ __forceinline__ void run(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR],
+                                               const uint4* tab1, const uint32_t (&cur)[20], const FIN& fin) {
+        using S = HalfSeq<T>;
+        constexpr int e = S::at(G), half = e >> 8, kb = (e >> 4) & 15, gi = e & 15, rb = kb - S::SH;
+        constexpr bool more = G + 1 < S::total();
+        uint32_t nxt[20];
+        if constexpr (more) {
+            constexpr int kb2 = (S::at(G + 1) >> 4) & 15, gi2 = S::at(G + 1) & 15;
+            load_table_lds(nxt, tab1 + ((1 << T) - (1 << (T - kb2)) + gi2) * 5);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < (1 << rb); j++) {
+            if (rb > 0 && (j & 1) != half) continue;
+            const int m = (gi << (rb + 1)) + j, m2 = m + (1 << rb);
+            L[m2] ^= L[m];
+            H[m2] ^= H[m];
+            mul_xor(L[m], H[m], L[m2], H[m2], cur);
+            asm volatile("" : "+v"(L[m]), "+v"(H[m]), "+v"(L[m2]), "+v"(H[m2]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (more) {
+            if constexpr (half == 0 && (S::at(G + 1) >> 8) == 1) fin(L, H);  // the even rows are final
+            HalfLoop<T, G + 1, FIN>::run(L, H, tab1, nxt, fin);
+        }
+    }
+};
+template <int T, class FIN>
+__device__ __forceinline__ void ifft_b_halves(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const uint4* tab1,
+                                              const FIN& fin) {
+    constexpr int e = HalfSeq<T>::at(0), kb = (e >> 4) & 15, gi = e & 15;
+    uint32_t t0[20];
+    load_table_lds(t0, tab1 + ((1 << T) - (1 << (T - kb)) + gi) * 5);
+    HalfLoop<T, 0, FIN>::run(L, H, tab1, t0, fin);
+}
+// fin of ifft_b_halves: the even rows
+template <int P, int T> struct EvenStore {
+    const PassArgs& a;
+    const Thr& cs;
+    __device__ __forceinline__ void operator()(const uint32_t (&L)[Geo<T>::NR], const uint32_t (&H)[Geo<T>::NR]) const {
+#pragma unroll
+        for (int m = 0; m < Geo<T>::NR; m += 2) {
+            if (a.voff32) store_row<P, T, true>(a, cs, L[m], H[m], m, nullptr, nullptr);
+            else store_row<P, T, false>(a, cs, L[m], H[m], m, nullptr, nullptr);
+        }
+    }
+};
+
 template <int P, int T>
 __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, uint32_t tile, uint32_t slab,
                                              ItemRegs<P, T>& d, uint8_t* smem) {
@@ -1214,6 +1297,8 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     // the output-pruned DEC_MID; the reveal stores measured slower inside it)
     constexpr bool EARLY = LayerSeq<T, false, 0, R, true>::DF && P != DEC_MID && PT::STORE != ST_RESTORE && PT::FFT &&
                            T > 4;
+    // the IFFT-only passes: early stores of the even rows (ifft_b_halves)
+    constexpr bool EARLY_B = PT::IFFT && !PT::FFT && PT::STORE == ST_PLAIN && T > 4 && G::R == 4 && !RS16_NO_EARLY_B;
     uint2* lds = (uint2*)smem;
     const uint4* tab1 = (const uint4*)(smem + SM::TAB1_OFF);
     const uint4* tab2 = (const uint4*)(smem + SM::TAB2_OFF);
@@ -1294,8 +1379,14 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                     }
                 });
             RS16_STAMP(a, 4);
-            layers<P, T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
-                                                                                                tab2, d.zmask);
+            if constexpr (EARLY_B) {
+                Thr cs = c;
+                asm volatile("" : "+v"(cs.offL));
+                ifft_b_halves<T>(L, H, tab1, EvenStore<P, T>{a, cs});
+            } else {
+                layers<P, T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
+                                                                                                    tab2, d.zmask);
+            }
             in_b = true;
         }
         RS16_STAMP(a, 5);
@@ -1388,8 +1479,17 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
     cs.b_high = uni(cs.b_high);
     asm volatile("" : "+s"(cs.b_low), "+s"(cs.b_high));
     asm volatile("" : "+v"(cs.offL));
-    if (a.voff32) store_rows<P, T, true>(a, cs, L, H, rvt, lostf);
-    else store_rows<P, T, false>(a, cs, L, H, rvt, lostf);
+    if constexpr (EARLY_B) {
+        // (the even rows went out inside the last block)
+#pragma unroll
+        for (int m = 1; m < NR; m += 2) {
+            if (a.voff32) store_row<P, T, true>(a, cs, L[m], H[m], m, rvt, lostf);
+            else store_row<P, T, false>(a, cs, L[m], H[m], m, rvt, lostf);
+        }
+    } else {
+        if (a.voff32) store_rows<P, T, true>(a, cs, L, H, rvt, lostf);
+        else store_rows<P, T, false>(a, cs, L, H, rvt, lostf);
+    }
     RS16_STAMP(a, 10);
     RS16_STAMP_END(a);
 }
