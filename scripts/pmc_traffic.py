@@ -21,6 +21,7 @@ WORK = {
     "bench": "32768:32768:1024",
     "extra": {"DEC_FIRST/T8": "32768:32768:1024 1% loss", "DEC_MID/T8": "32768:32768:1024 1% loss",
               "rs16::tile_last_kernel": "32768:32768:1024 1% loss",
+              "rs16::mid_direct_kernel": "32768:32768:1024 1% loss",
               "col2_kernel<L10,ENC>": "1000:1000:1024 encode",
               "col2_kernel<L10,DEC_EVAL>": "1000:1000:1024 100% loss",
               "col2_kernel<L11,DEC_GEN>": "1000:1000:1024 1% loss"},
