@@ -892,6 +892,12 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     if constexpr (!DEC) dma_tables();
     [[maybe_unused]] uint32_t ev[2] = {0, 0};
     [[maybe_unused]] bool lost[2] = {false, false};  // (GEN: the row is a lost original)
+    // GEN: a wave's rows in the maps S(k) are one 128-row block (wave index =
+    // row bits 7 ..); a block with no received row is zero through the
+    // IFFT's layers 0 .. 6 (ilive: they are skipped), a block with no lost
+    // original feeds no stored row from the FFT's layer 6 on (flive: skipped
+    // with the reveal).  Uniform branches.
+    bool ilive = true, flive = true;
     if constexpr (DEC) {
         bool rcv[2];
 #pragma unroll
@@ -903,6 +909,10 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
                 rcv[m] = !a.flags_o || fr[m] != 0;
                 if (!a.rev_a) lost[m] = !rcv[m];
             }
+        }
+        if constexpr (GEN) {
+            ilive = __ballot(rcv[0] || rcv[1]) != 0;
+            flive = __ballot(lost[0] || lost[1]) != 0;
         }
         uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
         ce.prep(a);
@@ -938,7 +948,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         __syncthreads();
     } else {
     // ---- IFFT layers 0 .. 6 in registers and lanes
-    bfly2<false>(XL, XH, i0);
+    if (ilive) bfly2<false>(XL, XH, i0);
     __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
     __syncthreads();
     RS16_STAMP(a, 2);
@@ -946,24 +956,29 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         tab2_img<L, 0, S0>(f0, t, img_fft);
         tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, img_fft);
     }
-    tab2<L, false, 2, S2>(wa, t, smem);
-    swap2<0>(XL, XH);
-    bfly2<false>(XL, XH, i1);
-    tab2<L, false, 3, S3>(wb, t, smem);
-    swap2<1>(XL, XH);
-    bfly2<false>(XL, XH, wa);
-    tab2<L, false, 4, S4>(wa, t, smem);
-    swap2<2>(XL, XH);
-    bfly2<false>(XL, XH, wb);
-    tab2<L, false, 5, S5>(wb, t, smem);
-    swap2<3>(XL, XH);
-    bfly2<false>(XL, XH, wa);
-    tab2<L, false, 6, S6>(wa, t, smem);
-    swap2<4>(XL, XH);
-    bfly2<false>(XL, XH, wb);
-    tab2<L, false, 7, MM>(wb, t, smem);
-    swap2<5>(XL, XH);
-    bfly2<false>(XL, XH, wa);
+    if (ilive) {
+        tab2<L, false, 2, S2>(wa, t, smem);
+        swap2<0>(XL, XH);
+        bfly2<false>(XL, XH, i1);
+        tab2<L, false, 3, S3>(wb, t, smem);
+        swap2<1>(XL, XH);
+        bfly2<false>(XL, XH, wa);
+        tab2<L, false, 4, S4>(wa, t, smem);
+        swap2<2>(XL, XH);
+        bfly2<false>(XL, XH, wb);
+        tab2<L, false, 5, S5>(wb, t, smem);
+        swap2<3>(XL, XH);
+        bfly2<false>(XL, XH, wa);
+        tab2<L, false, 6, S6>(wa, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<false>(XL, XH, wb);
+        tab2<L, false, 7, MM>(wb, t, smem);
+        swap2<5>(XL, XH);
+        bfly2<false>(XL, XH, wa);
+    } else {
+        // (a zero block stays zero in any row map)
+        tab2<L, false, 7, MM>(wb, t, smem);
+    }
     RS16_STAMP(a, 3);
     }
     // ---- layers 7 .. L-1 both ways around the middle, map M (GEN: the
@@ -1075,32 +1090,34 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     // (each thread writes the image rows it read in the first exchange: no
     // barrier; GEN: the derivative's image reads are behind a barrier above)
     exchange2<MM, S6>(XL, XH, t, img);
-    bfly2<true>(XL, XH, wb);  // FFT 6
-    tab2<L, true, 4, S4>(wb, t, smem);
-    swap2<5>(XL, XH);
-    bfly2<true>(XL, XH, wa);
-    tab2<L, true, 3, S3>(wa, t, smem);
-    swap2<4>(XL, XH);
-    bfly2<true>(XL, XH, wb);
-    tab2<L, true, 2, S2>(wb, t, smem);
-    swap2<3>(XL, XH);
-    bfly2<true>(XL, XH, wa);
-    swap2<2>(XL, XH);
-    bfly2<true>(XL, XH, wb);
-    swap2<1>(XL, XH);
-    bfly2<true>(XL, XH, f1);
     [[maybe_unused]] uint32_t rt[DEC ? 2 : 1][20];
-    if constexpr (DEC) {
+    if (flive) {
+        bfly2<true>(XL, XH, wb);  // FFT 6
+        tab2<L, true, 4, S4>(wb, t, smem);
+        swap2<5>(XL, XH);
+        bfly2<true>(XL, XH, wa);
+        tab2<L, true, 3, S3>(wa, t, smem);
+        swap2<4>(XL, XH);
+        bfly2<true>(XL, XH, wb);
+        tab2<L, true, 2, S2>(wb, t, smem);
+        swap2<3>(XL, XH);
+        bfly2<true>(XL, XH, wa);
+        swap2<2>(XL, XH);
+        bfly2<true>(XL, XH, wb);
+        swap2<1>(XL, XH);
+        bfly2<true>(XL, XH, f1);
+        if constexpr (DEC) {
 #pragma unroll
-        for (int m = 0; m < 2; m++) glb_table(rt[m], a.mul_tab, GF_MODULUS - ev[m]);
+            for (int m = 0; m < 2; m++) glb_table(rt[m], a.mul_tab, GF_MODULUS - ev[m]);
+        }
+        swap2<0>(XL, XH);
+        bfly2<true>(XL, XH, f0);
     }
-    swap2<0>(XL, XH);
-    bfly2<true>(XL, XH, f0);
     RS16_STAMP(a, 9);
     // ---- store rows < out_rows (DEC: revealed, rate_high.rs:236-242; GEN:
     // the lost originals only, restored in place)
 #pragma unroll
-    for (int m = 0; m < 2; m++) {
+    for (int m = 0; m < 2 && flive; m++) {
         const uint32_t r = S0::row(t, m);
         uint32_t vl = XL[m], vh = XH[m];
         if constexpr (DEC) {
