@@ -889,6 +889,8 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
             p[8] = XH[m];
         }
     };
+    // (a decoder's DMA comes after its per-row tables; issued before the eval
+    // instead, the general decode measured 0.2 us slower at 1000:1000)
     if constexpr (!DEC) dma_tables();
     [[maybe_unused]] uint32_t ev[2] = {0, 0};
     [[maybe_unused]] bool lost[2] = {false, false};  // (GEN: the row is a lost original)
@@ -916,25 +918,28 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         }
         uint32_t* elds = (uint32_t*)(smem + ColSmem<L>::ELOG);
         ce.prep(a);
+        RS16_STAMP(a, 1);
         ce.run(a, elds);
         __syncthreads();
+        RS16_STAMP(a, 2);
         uint32_t gt[2][20];
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             const uint32_t r = S0::row(t, m);
-            glb_table(gt[m], a.mul_tab, rcv[m] ? elds[a.base_in + r] : ZERO_ENTRY);
+            // (a zero block's rows need no table: the ZERO_ENTRY product is 0)
+            if (ilive) glb_table(gt[m], a.mul_tab, rcv[m] ? elds[a.base_in + r] : ZERO_ENTRY);
             ev[m] = elds[a.base_out + r];
         }
         dma_tables();
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             uint32_t zl = 0, zh = 0;
-            mul_xor(zl, zh, XL[m], XH[m], gt[m]);
+            if (ilive) mul_xor(zl, zh, XL[m], XH[m], gt[m]);
             XL[m] = zl;
             XH[m] = zh;
         }
     }
-    RS16_STAMP(a, 1);
+    RS16_STAMP(a, 3);
     // Each layer's LDS table is read one layer ahead (wa / wb), so its
     // latency hides under the previous layer's swap and butterfly.
     uint8_t* img = smem + ColSmem<L>::IMG;
@@ -951,10 +956,12 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     if (ilive) bfly2<false>(XL, XH, i0);
     __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
     __syncthreads();
-    RS16_STAMP(a, 2);
+    RS16_STAMP(a, 4);
     if constexpr (L <= 10 && !IFO) {
-        tab2_img<L, 0, S0>(f0, t, img_fft);
-        tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, img_fft);
+        if (flive) {
+            tab2_img<L, 0, S0>(f0, t, img_fft);
+            tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, img_fft);
+        }
     }
     if (ilive) {
         tab2<L, false, 2, S2>(wa, t, smem);
@@ -979,7 +986,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         // (a zero block stays zero in any row map)
         tab2<L, false, 7, MM>(wb, t, smem);
     }
-    RS16_STAMP(a, 3);
+    RS16_STAMP(a, 5);
     }
     // ---- layers 7 .. L-1 both ways around the middle, map M (GEN: the
     // formal derivative between the IFFT's last layer and the FFT's first)
@@ -1012,8 +1019,10 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         swap2<3>(XL, XH);
         bfly2<true>(XL, XH, wa);   // FFT 7
         // (at 16 waves the FFT's layer-0/1 tables are requested here: 128 VGPRs)
-        tab2_img<L, 0, S0>(f0, t, a.img_fft);
-        tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, a.img_fft);
+        if (flive) {
+            tab2_img<L, 0, S0>(f0, t, a.img_fft);
+            tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, a.img_fft);
+        }
         __syncthreads();  // (every wave has read its derivative terms from the image)
     } else if constexpr (L == 10) {
         using S8 = typename SMap<L, 8>::M;
@@ -1085,7 +1094,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         bfly2<true>(XL, XH, wa);   // FFT 7
         if constexpr (GEN) __syncthreads();
     }
-    RS16_STAMP(a, 4);
+    RS16_STAMP(a, 6);
     tab2<L, true, 5, S5>(wa, t, smem);
     // (each thread writes the image rows it read in the first exchange: no
     // barrier; GEN: the derivative's image reads are behind a barrier above)
