@@ -275,9 +275,11 @@ template <int L, int PTS, int NT_ = (1 << L) / 4> struct ColEval {
         const uint32_t t = threadIdx.x;
         int* sx = (int*)elds;
         fwht_points<NT, PTS>(x, sx);
+        RS16_STAMP(a, 2);
 #pragma unroll
         for (int j = 0; j < PTS; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
         fwht_points<NT, PTS>(x, sx);
+        RS16_STAMP(a, 3);
 #pragma unroll
         for (int j = 0; j < PTS; j++) elds[t + NT * j] = mod65535(x[j] + (int)a.e_k);
     }
@@ -847,10 +849,14 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     // the IFFT: the prologue is bound by the CU's L2 bandwidth, and a thread's
     // own tables for layers 0 and 1 are most of its bytes)
     uint32_t i0[20], i1[20], f0[20], f1[20];
+    // GEN: requested with the per-row tables after the eval, by the waves
+    // whose block is live (the eval's first barrier would wait for every
+    // wave's table requests; 1 %-loss 1000:1000 decode 16.1 -> 15.4 us)
+    constexpr bool LATE_I01 = GEN;
     if constexpr (FFX) {
         tab2_img<L, 0, S0>(f0, t, img_fft);
         tab2_img<L, 1, typename SMap<L, 1>::M>(f1, t, img_fft);
-    } else {
+    } else if constexpr (!LATE_I01) {
         tab2_img<L, 0, S0>(i0, t, img_ifft);
         tab2_img<L, 1, typename SMap<L, 1>::M>(i1, t, img_ifft);
     }
@@ -921,8 +927,14 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         RS16_STAMP(a, 1);
         ce.run(a, elds);
         __syncthreads();
-        RS16_STAMP(a, 2);
+        RS16_STAMP(a, 4);
         uint32_t gt[2][20];
+        if constexpr (LATE_I01) {
+            if (ilive) {
+                tab2_img<L, 0, S0>(i0, t, img_ifft);
+                tab2_img<L, 1, typename SMap<L, 1>::M>(i1, t, img_ifft);
+            }
+        }
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             const uint32_t r = S0::row(t, m);
@@ -939,7 +951,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
             XH[m] = zh;
         }
     }
-    RS16_STAMP(a, 3);
+    RS16_STAMP(a, 5);
     // Each layer's LDS table is read one layer ahead (wa / wb), so its
     // latency hides under the previous layer's swap and butterfly.
     uint8_t* img = smem + ColSmem<L>::IMG;
@@ -956,7 +968,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     if (ilive) bfly2<false>(XL, XH, i0);
     __builtin_amdgcn_s_waitcnt(0);  // (the LDS-DMA loads of layers >= 2 have landed)
     __syncthreads();
-    RS16_STAMP(a, 4);
+    RS16_STAMP(a, 6);
     if constexpr (L <= 10 && !IFO) {
         if (flive) {
             tab2_img<L, 0, S0>(f0, t, img_fft);
@@ -986,7 +998,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         // (a zero block stays zero in any row map)
         tab2<L, false, 7, MM>(wb, t, smem);
     }
-    RS16_STAMP(a, 5);
+    RS16_STAMP(a, 7);
     }
     // ---- layers 7 .. L-1 both ways around the middle, map M (GEN: the
     // formal derivative between the IFFT's last layer and the FFT's first)
@@ -1094,7 +1106,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
         bfly2<true>(XL, XH, wa);   // FFT 7
         if constexpr (GEN) __syncthreads();
     }
-    RS16_STAMP(a, 6);
+    RS16_STAMP(a, 8);
     tab2<L, true, 5, S5>(wa, t, smem);
     // (each thread writes the image rows it read in the first exchange: no
     // barrier; GEN: the derivative's image reads are behind a barrier above)
