@@ -51,6 +51,11 @@
 #include "rs16_colops.hpp"
 #include "rs16_diag.hpp"
 
+// (timing A/B builds: 0 = the radix-2 decoder's eval with 16-term wave layers)
+#ifndef RS16_COL_EVAL_XP
+#define RS16_COL_EVAL_XP 1
+#endif
+
 namespace rs16 {
 
 namespace {
@@ -219,6 +224,75 @@ template <int NT, int PTS> __device__ __forceinline__ void fwht_points(int (&x)[
     }
 }
 
+// The same transform with its wave layers as lane layers (XP forms of
+// ColEval, the radix-2 kernel): the points go once through LDS to layout X,
+// where the wave bits of the thread index and its lane bits 0 .. WB-1 trade
+// places, and back.  The wave layers of the 16-wave workgroups read 16
+// values per point (fwht_points); here a point is read once per transpose.
+// LDS addresses XOR-swizzled (bank = p ^ (p >> 6)): conflict-free both ways.
+template <int NT> struct XLay {
+    static constexpr int WB = NT >= 1024 ? 4 : NT >= 512 ? 3 : NT >= 256 ? 2 : NT >= 128 ? 1 : 0;
+    static constexpr uint32_t LM = (1u << WB) - 1;
+    // the point of thread t's register j in layout X (layout O: t + NT j)
+    static __device__ __forceinline__ uint32_t px(uint32_t t, int j) {
+        const uint32_t lane = t & 63, w = t >> 6;
+        return w | (lane & 63u & ~LM) | ((lane & LM) << 6) | (uint32_t)j * NT;
+    }
+    static __device__ __forceinline__ uint32_t sw(uint32_t p) { return p ^ ((p >> 6) & 63u); }
+};
+// register layers, then lane layers of lane bits [B0, B1)
+template <int PTS, int B0, int B1, bool REG> __device__ __forceinline__ void fwht_lanes(int (&x)[PTS]) {
+    const uint32_t lane = threadIdx.x & 63;
+    if constexpr (REG) {
+#pragma unroll
+        for (int d = 1; d < PTS; d <<= 1)
+#pragma unroll
+            for (int j = 0; j < PTS; j++)
+                if (!(j & d)) {
+                    const int u = x[j], v = x[j + d];
+                    x[j] = u + v;
+                    x[j + d] = u - v;
+                }
+    }
+#define RS16_LANE(B)                                              \
+    if constexpr ((B) >= B0 && (B) < B1) {                        \
+        _Pragma("unroll") for (int j = 0; j < PTS; j++) {         \
+            const int p = xshfl<(1 << (B))>(x[j]);                \
+            x[j] = (lane & (1u << (B))) ? p - x[j] : x[j] + p;    \
+        }                                                         \
+    }
+    RS16_LANE(0) RS16_LANE(1) RS16_LANE(2) RS16_LANE(3)
+#undef RS16_LANE
+#pragma unroll
+    for (int lb = 4; lb <= 5; lb++) {
+        if (lb < B0 || lb >= B1) continue;
+#pragma unroll
+        for (int j = 0; j < PTS; j += 2) {
+            auto swp = [&]() {
+                const auto r = lb == 4 ? __builtin_amdgcn_permlane16_swap((uint32_t)x[j], (uint32_t)x[j + 1], false, false)
+                                       : __builtin_amdgcn_permlane32_swap((uint32_t)x[j], (uint32_t)x[j + 1], false, false);
+                x[j] = (int)r[0];
+                x[j + 1] = (int)r[1];
+            };
+            swp();
+            const int u = x[j], v = x[j + 1];
+            x[j] = u + v;
+            x[j + 1] = u - v;
+            swp();
+        }
+    }
+}
+// layout O -> X (TO_X) or X -> O through sx; barrier after the writes
+template <int NT, int PTS, bool TO_X> __device__ __forceinline__ void fwht_xpose(int (&x)[PTS], int* sx) {
+    using X = XLay<NT>;
+    const uint32_t t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < PTS; j++) sx[X::sw(TO_X ? t + NT * j : X::px(t, j))] = x[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PTS; j++) x[j] = sx[X::sw(TO_X ? X::px(t, j) : t + NT * j)];
+}
+
 // The erasure logs of work rows [0, NT PTS) into elds, and the received
 // counts per 64-row chunk (rcount, workgroup 0) for rs16_decode_check.
 // Segment A = recovery rows [0, in_rows) (flags), [in_rows, chunk) padding
@@ -229,7 +303,7 @@ template <int NT, int PTS> __device__ __forceinline__ void fwht_points(int (&x)[
 // thread's points) -- the kernel calls it before its row loads and table
 // DMA, so that waiting for them does not wait for the DMA (vmcnt counts in
 // issue order) -- and run() computes.
-template <int L, int PTS, int NT_ = (1 << L) / 4> struct ColEval {
+template <int L, int PTS, int NT_ = (1 << L) / 4, bool XP = false> struct ColEval {
     static constexpr int N = 1 << L, NT = NT_;
     uint8_t f[PTS];
     uint32_t vt[PTS];
@@ -241,7 +315,7 @@ template <int L, int PTS, int NT_ = (1 << L) / 4> struct ColEval {
             const bool in_a = p < a.in_rows, in_b = p >= a.chunk && p - a.chunk < a.o_rows;
             const uint8_t* fp = in_a && a.flags ? a.flags + p : (in_b && a.flags_o ? a.flags_o + (p - a.chunk) : a.zero);
             f[j] = *(const __attribute__((address_space(1))) uint8_t*)fp;
-            vt[j] = a.vtab[p];
+            vt[j] = a.vtab[XP ? XLay<NT>::px(t, j) : p];  // (XP: the product is taken in layout X)
         }
     }
     // the erasure vector of the thread's points (and the received counts):
@@ -274,6 +348,24 @@ template <int L, int PTS, int NT_ = (1 << L) / 4> struct ColEval {
     __device__ __forceinline__ void run(const ColArgs& a, uint32_t* elds) {
         const uint32_t t = threadIdx.x;
         int* sx = (int*)elds;
+        if constexpr (XP) {
+            constexpr int WB = XLay<NT>::WB;
+            // H(e): every bit but the wave bits in layout O, those in X
+            fwht_lanes<PTS, 0, 6, true>(x);
+            fwht_xpose<NT, PTS, true>(x, sx);
+            fwht_lanes<PTS, 0, WB, false>(x);
+#pragma unroll
+            for (int j = 0; j < PTS; j++) x[j] = (int)fold65535(mod65535(x[j]) * vt[j]);
+            // H(.): every bit but point bits [0, WB) in X, those in O
+            fwht_lanes<PTS, 0, 6, true>(x);
+            __syncthreads();  // (every thread has read its X points)
+            fwht_xpose<NT, PTS, false>(x, sx);
+            __syncthreads();  // (elds overwrites sx)
+            fwht_lanes<PTS, 0, WB, false>(x);
+#pragma unroll
+            for (int j = 0; j < PTS; j++) elds[t + NT * j] = mod65535(x[j] + (int)a.e_k);
+            return;
+        }
         fwht_points<NT, PTS>(x, sx);
         RS16_STAMP(a, 2);
 #pragma unroll
@@ -834,7 +926,7 @@ __global__ __launch_bounds__((1 << L) / 2) void col2_kernel(ColArgs a) {
     // ---- requests, as col_kernel: the decoder's flags and polynomial
     // inputs first, then the layer-0/1 tables into registers, the rows, the DMA
     [[maybe_unused]] uint8_t fr[2] = {0, 0};
-    [[maybe_unused]] ColEval<L, (DEC ? (GEN ? N : 2 * N) / NT : 1), NT> ce;
+    [[maybe_unused]] ColEval<L, (DEC ? (GEN ? N : 2 * N) / NT : 1), NT, RS16_COL_EVAL_XP> ce;
     if constexpr (DEC) {
 #pragma unroll
         for (int m = 0; m < 2; m++) {
