@@ -258,12 +258,14 @@ def test_col_decode_check_counts(eng, k, m):
                                  (1000, 1000), (1000, 100), (1024, 1024), (600, 1000), (1500, 500),
                                  # low rate (originals = segment A, erasure tail of ones)
                                  (100, 1000), (60, 1000), (200, 700)])
-@pytest.mark.parametrize("pattern", ["1pct", "random", "mixed"])
+@pytest.mark.parametrize("pattern", ["1pct", "random", "mixed", "tail_rec", "two_blocks"])
 def test_col_general_decode(eng, k, m, pattern, form):
     """The general decode (any loss pattern) of up to 2048 work rows in one
     launch: polynomial, gather of both segments, IFFT, formal derivative, FFT,
     reveal (rate_high.rs:168-247); every lost original restored bit for bit,
-    received originals untouched."""
+    received originals untouched.  tail_rec / two_blocks: the radix-2
+    kernel's per-wave skips (128-row blocks with no received row, with no
+    lost original) at other blocks than the reference pattern's."""
     sb = 64
     original = generate_original(k, sb, 3 * k + m)
     recovery = O.encode(k, m, original)
@@ -273,6 +275,16 @@ def test_col_general_decode(eng, k, m, pattern, form):
         loss = max(1, min(k, m) // 100)
         om[k - loss:] = False
         rm[:loss] = True
+    elif pattern == "tail_rec":  # the last recovery shards, lost originals at the front
+        loss = max(1, min(k, m) // 50)
+        om[:loss] = False
+        rm[m - loss:] = True
+    elif pattern == "two_blocks":  # lost originals in two distant 128-row blocks
+        loss = max(2, min(k, m) // 40)
+        half = loss // 2
+        om[:half] = False
+        om[k - (loss - half):] = False
+        rm[rng.choice(m, min(m, loss + 1), replace=False)] = True
     else:
         loss = int(rng.integers(1, min(k, m) + 1)) if pattern == "random" else min(k, m) // 2
         om[rng.choice(k, loss, replace=False)] = False
