@@ -24,6 +24,8 @@ On top of that every case draws what this engine's path choice depends on:
     formal derivative through LDS, the evaluated erasure logs of whole-half erasures.
 Every case's parameters are in the assertion message.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -37,6 +39,10 @@ DIAGS = (rs16.DIAG_FORCE_VOFF64, rs16.DIAG_EVAL_TWO_KERNEL, rs16.DIAG_EVAL_FULL,
          rs16.DIAG_FORCE_COLUMN, rs16.DIAG_TILE_LAST, rs16.DIAG_NO_TILE_LAST, rs16.DIAG_FD_LDS,
          rs16.DIAG_COL_RADIX4, rs16.DIAG_NO_IDENTITY, rs16.DIAG_NO_MID_DIRECT)
 BUDGET = 3 << 20  # bytes of originals + recovery per case (all stripes)
+# soak runs (not the default suite): RS16_FUZZ_SEED shifts every test's seed,
+# RS16_FUZZ_MULT multiplies its case count
+SEED = int(os.environ.get("RS16_FUZZ_SEED", "0"))
+MULT = max(1, int(os.environ.get("RS16_FUZZ_MULT", "1")))
 
 
 def next_pow2(x):
@@ -87,9 +93,9 @@ def eng():
 def test_random_rate_api(eng):
     """The Rate API (ReedSolomonEncoder / Decoder and the forced rates) with
     coders reused across cases, random widths and switches: 60 cases."""
-    rng = np.random.default_rng(20240611)
+    rng = np.random.default_rng(20240611 + SEED)
     coders = {}
-    for case in range(60):
+    for case in range(60 * MULT):
         k, m = random_counts(rng)
         sb = random_width(rng, k + m)
         diag = random_diag(rng)
@@ -131,8 +137,8 @@ def _decode_masks(eng, k, m, o_lost, r_lost):
 def test_random_device_oneshot(eng):
     """rs16_encode_device / rs16_decode_device with 1-4 column slices:
     80 cases, lost slots holding garbage."""
-    rng = np.random.default_rng(7_000_001)
-    for case in range(80):
+    rng = np.random.default_rng(7_000_001 + SEED)
+    for case in range(80 * MULT):
         k, m = random_counts(rng)
         sb = random_width(rng, k + m)
         diag = random_diag(rng)
@@ -164,8 +170,8 @@ def test_random_device_oneshot(eng):
 def test_random_batches(eng):
     """rs16_encode_device_batch + rs16_decode_device_batch (one shared loss
     pattern): 2-12 stripes with gaps between them, 40 cases."""
-    rng = np.random.default_rng(31_337)
-    for case in range(40):
+    rng = np.random.default_rng(31_337 + SEED)
+    for case in range(40 * MULT):
         k, m = random_counts(rng)
         n = int(rng.integers(2, 13))
         sb = 64 * int(rng.integers(1, max(1, min(128, BUDGET // (64 * (k + m) * n))) + 1))
@@ -205,8 +211,8 @@ def test_random_batches(eng):
 def test_random_batches_varied(eng):
     """rs16_decode_device_batch_varied: every stripe its own loss set drawn
     by the reference's rules, 2-12 stripes, 40 cases."""
-    rng = np.random.default_rng(4_242_424)
-    for case in range(40):
+    rng = np.random.default_rng(4_242_424 + SEED)
+    for case in range(40 * MULT):
         k, m = random_counts(rng)
         n = int(rng.integers(2, 13))
         sb = 64 * int(rng.integers(1, max(1, min(128, BUDGET // (64 * (k + m) * n))) + 1))
