@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--no-extra", action="store_true", help="skip the 1000:1000 side measurements")
     p.add_argument("--no-verify", action="store_true", help="diagnostic (ablation) builds only")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    p.add_argument("--cpu-stub", action="store_true",
+                   help="tests only: no GPU, a numpy stand-in step through the multi-rank control plane")
     return p.parse_args()
 
 
@@ -355,7 +357,8 @@ def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
     step()
     n4 = max(3, steps // 4)
     t_all = timed(step, n4)
-    t_codec = timed(codec, n4)
+    codec_rank = []
+    t_codec = timed(codec, n4, codec_rank)
     t_coll = timed(lambda: (scatter_orig(), gather_rec(), scatter_rec(), gather_out()), n4)
     # Each collective on its own: the bytes that cross
     # the links (every column but the root's own slice: rows x (S - w_root)),
@@ -386,6 +389,7 @@ def configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, steps):
                     f"({w} B each) with RCCL scatter/gather; encode + 100%-loss decode (BASELINE configs[4])",
         "gib_s": step_bytes * n4 / t_all / GIB, "ms_per_step": t_all / n4 * 1e3,
         "codec_only_gib_s": step_bytes * n4 / t_codec / GIB, "codec_only_ms": t_codec / n4 * 1e3,
+        "codec_ms_per_rank": [round(t / n4 * 1e3, 4) for t in codec_rank],
         "collectives_ms": t_coll / n4 * 1e3,
         # scatter originals (k rows) + gather recovery (m) + scatter recovery (m)
         # + gather originals (k), each moving every column but the root's own slice
@@ -404,10 +408,13 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
     encoding a stripe while engine B decodes another one's (already encoded)
     recovery.  Both restorations are checked.
 
-    Some stream pairs share a hardware queue and then run one stripe after
-    the other (scripts/probe_queues.py): the second engine is
-    taken from up to 4 candidates, the first whose pair overlaps (two stripes
-    in < 1.6 x the time of one); the first candidate's rate is reported too."""
+    Two streams that share a hardware queue run one stripe after the other
+    (scripts/probe_queues.py, profiles/r05_queues.txt).  The second engine is
+    created with RS16_ENGINE_OWN_QUEUE (include/rs16.h: its stream gets a
+    hardware queue of its own), so the pair overlaps by construction: ONE
+    engine, no selection among candidates.  A second engine created the
+    default way is measured beside it for comparison (`default_second_engine`):
+    whether that one overlaps depends on which queue the runtime gives it."""
     import numpy as np
 
     import rs16
@@ -434,10 +441,9 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
         decode()
 
     t1 = run([eng], one, 10, 3) / 10
-    tried = []
-    chosen = None
-    for cand in range(4):
-        eng2 = rs16.Engine(local)
+
+    def pair(flags):
+        eng2 = rs16.Engine(local, flags)
         a2, r2, x2 = DeviceArray.from_numpy(eng2, o2), DeviceArray(eng2, m * S), DeviceArray(eng2, k * S)
         f2o, f2r = DeviceArray.from_numpy(eng2, of), DeviceArray.from_numpy(eng2, rf)
         if loss < k:
@@ -455,36 +461,194 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
             decode()
             dec2()
 
+        def enc_dec():
+            encode()
+            dec2()
+
         two()
         eng2.synchronize()
         assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
-        ratio = run([eng, eng2], two, 10, 3) / 10 / t1
-        tried.append(round(ratio, 3))
-        if ratio < 1.6 or cand == 3:
-            chosen = (eng2, a2, r2, x2, f2o, f2r, enc2, dec2, two)
-            break
+        t2 = run([eng, eng2], two, args.steps, args.warmup)
+        t3 = run([eng, eng2], enc_dec, args.steps, args.warmup)
+        assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
         del a2, r2, x2, f2o, f2r
         eng2.close()
-    eng2, a2, r2, x2, f2o, f2r, enc2, dec2, two = chosen
+        return t2, t3
 
-    def enc_dec():
-        encode()
-        dec2()
-
-    t2 = run([eng, eng2], two, args.steps, args.warmup)
-    t3 = run([eng, eng2], enc_dec, args.steps, args.warmup)
-    assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
-    del a2, r2, x2, f2o, f2r
-    eng2.close()
+    t2, t3 = pair(rs16.Engine.OWN_QUEUE)
+    t2d, t3d = pair(0)
     return {"gib_s": 2 * step_bytes * args.steps / t2 / GIB, "ms_per_two_stripes": t2 / args.steps * 1e3,
             "encode_while_decode_gib_s": step_bytes * args.steps / t3 / GIB,
             "encode_while_decode_us": t3 / args.steps * 1e6, "where": where,
-            "second_engine_candidates": tried,
-            "first_candidate_gib_s": 2 * step_bytes / (tried[0] * t1) / GIB,
+            "one_stripe_gib_s": step_bytes / t1 / GIB,
+            "two_stripe_time_over_one": round(t2 / args.steps / t1, 3),
+            "second_engine": "rs16_engine_new_ex(RS16_ENGINE_OWN_QUEUE): one engine, no selection",
+            "default_second_engine": {"gib_s": 2 * step_bytes * args.steps / t2d / GIB,
+                                      "encode_while_decode_gib_s": step_bytes * args.steps / t3d / GIB,
+                                      "two_stripe_time_over_one": round(t2d / args.steps / t1, 3),
+                                      "note": "second engine from rs16_engine_new: its stream's hardware queue is "
+                                              "the runtime's choice (a shared queue runs the pair serially, ~2.0)"},
             "note": "serving-mode throughput: two independent 32768:32768 x 1 KiB stripes in flight "
                     "(gib_s), or one stripe encoding on engine A while another's recovery decodes on "
-                    "engine B (encode_while_decode); candidates = two-stripe time / one-stripe time per "
-                    "second engine tried (a pair on one hardware queue runs serially, ~2.0); not the metric"}
+                    "engine B (encode_while_decode); not the metric"}
+
+
+def make_timed(sync, dist, world):
+    """timed(fn, steps[, per_rank]): run fn `steps` times between two
+    barriers (device sync + gloo barrier) and return the MAX over ranks of the
+    wall time; `per_rank` (a list) receives every rank's own time, in rank
+    order, so that a straggler of a multi-GPU run can be named."""
+    def barrier():
+        sync()
+        if dist is not None:
+            dist.barrier()
+
+    def timed(fn, steps, per_rank=None):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        sync()
+        dt = time.perf_counter() - t0
+        barrier()
+        if dist is not None:
+            import torch
+            t = torch.tensor([dt], dtype=torch.float64)
+            if per_rank is not None:
+                allt = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+                dist.all_gather(allt, t)
+                per_rank[:] = [float(x.item()) for x in allt]
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        elif per_rank is not None:
+            per_rank[:] = [dt]
+        return dt
+
+    return timed, barrier
+
+
+def rank_identity(local, device):
+    """Who this rank is: host, local rank, the HIP device index it runs on and
+    the visible-device list the launcher gave it."""
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES") or \
+        os.environ.get("CUDA_VISIBLE_DEVICES")
+    return {"hostname": socket.gethostname(), "local_rank": local, "device": device, "visible_devices": vis,
+            "pid": os.getpid()}
+
+
+def gather_ranks(dist, world, ident, per_rank_dt, steps, rank_bytes):
+    """Per-rank rows of the timed loop for the JSON line (rank order): the
+    rank's identity, its own time per step and its own GiB/s.  The metric
+    itself stays world x bytes / max-over-ranks time."""
+    idents = [ident]
+    if dist is not None:
+        idents = [None] * world
+        dist.all_gather_object(idents, ident)
+    rows = []
+    for r, (who, dt) in enumerate(zip(idents, per_rank_dt)):
+        row = {"rank": r}
+        row.update(who)
+        row.update({"ms_per_step": round(dt / steps * 1e3, 4), "gib_s": round(rank_bytes * steps / dt / GIB, 3)})
+        rows.append(row)
+    return rows
+
+
+def stub_main(args, world, rank, local, dist, json_fd):
+    """--cpu-stub (tests only, no GPU): the multi-rank control plane of main()
+    -- barriers, max over ranks, per-rank rows, the configs4 per-rank codec
+    times -- around a numpy stand-in for the step, so that a CPU test can run
+    `bench.py --gpus 2` under gloo and check the line's fields.  The line says
+    "stub": it is never a measurement."""
+    import numpy as np
+
+    buf = np.random.default_rng(rank).integers(0, 256, 1 << 20, dtype=np.uint8)
+
+    def step():
+        np.bitwise_xor(buf, 0x5A, out=buf)
+
+    timed, _ = make_timed(lambda: None, dist, world)
+    per_rank = []
+    for _ in range(args.warmup):
+        step()
+    dt = timed(step, args.steps, per_rank)
+    codec_rank = []
+    timed(step, max(3, args.steps // 4), codec_rank)
+    step_bytes = 2 * buf.size
+    ranks = gather_ranks(dist, world, rank_identity(local, -1), per_rank, args.steps, step_bytes)
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(world * step_bytes * args.steps / dt / GIB, 3), "unit": "GiB/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt / args.steps * 1e3, 4), "stub": True, "ranks": ranks,
+               "extra": {"configs4_rccl": {"codec_ms_per_rank": [round(t * 1e3, 4) for t in codec_rank]}}}
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def general_decodes(eng, k, m, S, original, d_rec, timed, args, world):
+    """Decodes that take the general path: none of the
+    metric decode's shortcuts applies (whole-half erasure -> identity logs,
+    DESIGN.md 3.13; lost originals in <= 4 last-pass tiles -> direct middle
+    pass, 3.14), as the reference runs its one sequence for every pattern
+    (src/rate/rate_high.rs:181-242; random loss sets as
+    examples/test-random-roundtrips.rs:118-128):
+      scattered_1pct  - 327 random originals lost, 327 random recovery shards
+      random_50pct    - 16384 random originals lost, as many random recovery shards
+      30000:30000_100pct - every original lost, k = m not a power of two (no
+                        identity logs: eval_poly + both per-row multiplies)
+    Each: decode time (GiB/s over (k + m) S, as the metric counts a decode),
+    restore checked, and the per-program kernel times of a profiled run."""
+    import numpy as np
+
+    import rs16
+    from rs16.device import DeviceArray
+
+    rng = np.random.default_rng(11)
+    cases = {}
+    for name in ("scattered_1pct", "random_50pct", "30000:30000_100pct"):
+        kk, mm = k, m
+        if name == "30000:30000_100pct":
+            kk = mm = 30000
+        o = original[:kk]
+        lost = {"scattered_1pct": kk // 100, "random_50pct": kk // 2}.get(name, kk)
+        of = np.ones(kk, np.uint8)
+        rf = np.zeros(mm, np.uint8)
+        if lost == kk:
+            of[:] = 0
+            rf[:lost] = 1
+        else:
+            of[rng.choice(kk, lost, replace=False)] = 0
+            rf[rng.choice(mm, lost, replace=False)] = 1
+        if kk == k and mm == m:
+            rec = d_rec
+        else:
+            d_o = DeviceArray.from_numpy(eng, o)
+            rec = DeviceArray(eng, mm * S)
+            rs16.encode_device(kk, mm, S, d_o.ptr, rec.ptr, engine=eng)
+        held = o.copy()
+        held[of == 0] = 0
+        d_x = DeviceArray.from_numpy(eng, held)
+        d_of, d_rf = DeviceArray.from_numpy(eng, of), DeviceArray.from_numpy(eng, rf)
+        dec = lambda: rs16.decode_device(kk, mm, S, d_x.ptr, d_of.ptr, rec.ptr, d_rf.ptr, kk - lost, lost,
+                                         engine=eng)
+        dec()
+        assert np.array_equal(d_x.download(shape=(kk, S)), o), f"general decode {name} did not restore"
+        for _ in range(args.warmup):
+            dec()
+        n = max(10, args.steps)
+        t = timed(dec, n)
+        eng.set_profiling(True)
+        eng.profile_reset()
+        for _ in range(n):
+            dec()
+        eng.synchronize()
+        prof = eng.profile()
+        eng.set_profiling(False)
+        eng.profile_reset()
+        cases[name] = {"decode_us": t / n * 1e6, "decode_gib_s": world * (kk + mm) * S * n / t / GIB,
+                       "lost_originals": lost, "received_recovery": int(rf.sum()),
+                       "kernels_us": {p: round(ms / c * 1e3, 2) for p, (ms, c) in prof.items()}}
+    return cases
 
 
 def main():
@@ -509,10 +673,13 @@ def main():
         # librs16.so first: its RCCL (ROCm's, the one include/rs16.h's
         # rccl.h describes) must be the librccl.so.1 of this process, not the
         # copy torch brings along (a different RCCL version)
-        from rs16._lib import lib as _rs16_lib
-        _rs16_lib()
+        if not args.cpu_stub:
+            from rs16._lib import lib as _rs16_lib
+            _rs16_lib()
         import torch.distributed as dist  # control plane only (barrier, max of times)
         dist.init_process_group("gloo", init_method="env://")
+    if args.cpu_stub:
+        return stub_main(args, world, rank, local, dist, json_fd)
 
     import numpy as np
 
@@ -561,25 +728,7 @@ def main():
     if args.no_verify:
         verified = "NOT VERIFIED (diagnostic build)"
 
-    def barrier():
-        eng.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    def timed(fn, steps):
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            fn()
-        eng.synchronize()
-        dt = time.perf_counter() - t0
-        barrier()
-        if dist is not None:
-            import torch
-            t = torch.tensor([dt], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return dt
+    timed, barrier = make_timed(eng.synchronize, dist, world)
 
     # The step: encode the stripe, then decode its recovery at 100 % original
     # loss (encode, then rs16_decode_device, on the engine stream).  With
@@ -627,10 +776,12 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    dt = timed(step, args.steps)
+    per_rank_dt = []
+    dt = timed(step, args.steps, per_rank_dt)
     prof = eng.profile()
     step_bytes = 2 * (k + m) * S  # encode + decode, (original + recovery) bytes each
     value = world * step_bytes * args.steps / dt / GIB
+    ranks = gather_ranks(dist, world, rank_identity(local, eng.device), per_rank_dt, args.steps, step_bytes)
     ms_per_step = dt / args.steps * 1e3
 
     # Separate encode-only / decode-only rates (same data, same engine), and
@@ -809,6 +960,9 @@ def main():
         extra["decode_1pct_loss"] = {"decode_gib_s": world * (k + m) * S * args.steps / t1 / GIB,
                                      "decode_us": t1 / args.steps * 1e6, "lost_originals": L1,
                                      "received": f"originals 0..{k - L1}, recovery 0..{L1}"}
+
+    if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
+        extra["general_decodes"] = general_decodes(eng, k, m, S, original, d_rec, timed, args, world)
 
     if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
         # The multi-chunk rate paths: high rate with k > chunk
@@ -1004,6 +1158,7 @@ def main():
                                         if args.split_decode else "serial: rs16_decode_device after the encode")},
             "encode_gib_s": round(world * (k + m) * S * args.steps / dt_e / GIB, 3),
             "decode_gib_s": round(world * (k + m) * S * args.steps / dt_d / GIB, 3),
+            "ranks": ranks,
             "roofline": roofline,
             "valu_roofline": valu,
             "cpu_baseline": cpu,

@@ -75,6 +75,16 @@ size_t rs16_error_message(const rs16_error* err, char* buf, size_t len);
  * uploads them to the device's HBM. */
 typedef struct rs16_engine rs16_engine;
 rs16_engine* rs16_engine_new(int device, rs16_error* err);
+/* rs16_engine_new with creation flags (0 = rs16_engine_new).
+ * RS16_ENGINE_OWN_QUEUE: the engine's stream gets a hardware queue of its
+ * own (a stream with a CU mask enabling every CU; the HIP runtime shares its
+ * GPU_MAX_HW_QUEUES queues among unmasked streams only).  Two engines whose
+ * streams share a queue run one after the other; serving callers that keep
+ * two stripes in flight on two engines create the second one this way so the
+ * pair overlaps deterministically (profiles/r05_queues.txt).
+ * Unknown flags: RS16_INVALID_ARGUMENT. */
+enum { RS16_ENGINE_OWN_QUEUE = 1 };
+rs16_engine* rs16_engine_new_ex(int device, int flags, rs16_error* err);
 void rs16_engine_free(rs16_engine* eng);
 int rs16_engine_device(const rs16_engine* eng);
 void* rs16_engine_stream(const rs16_engine* eng);     /* hipStream_t owned by the engine */
@@ -483,6 +493,10 @@ enum {
                                       with the pass's matrix) */
 };
 int rs16_engine_set_diagnostics(rs16_engine* eng, int flags);
+/* Deprecated (the round-4 process-wide form, kept for existing callers):
+ * sets the flags every engine created AFTER the call starts with and returns
+ * the previous default.  Engines that exist keep their own flags. */
+int rs16_set_diagnostics(int flags);
 
 /* Diagnostics: host-side evaluation of the device multiply (same v_perm
  * byte-table format and code path as the kernels, with v_perm emulated):

@@ -2,6 +2,7 @@
 // encoder/decoder state machines (EncoderWork / DecoderWork semantics of
 // src/rate/{encoder,decoder}_work.rs) with HBM-resident work space, and the
 // device-resident one-shot codec.
+#include <atomic>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -141,13 +142,18 @@ extern "C" int rs16_decode_check(rs16_engine* e, void* stream, rs16_error* err) 
     if (got_o != want_o || got_r != want_r) return set_error(err, RS16_INVALID_ARGUMENT, got_o, got_r);
     return set_error(err, RS16_OK);
 }
+static constexpr int DIAG_ALL = DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN |
+                                DIAG_FORCE_COLUMN | DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS |
+                                DIAG_COL_RADIX4 | DIAG_NO_IDENTITY | DIAG_NO_MID_DIRECT;
 extern "C" int rs16_engine_set_diagnostics(rs16_engine* e, int flags) {
     const int old = e->diag;
-    e->diag = flags & (DIAG_FORCE_VOFF64 | DIAG_EVAL_TWO_KERNEL | DIAG_EVAL_FULL | DIAG_NO_COLUMN | DIAG_FORCE_COLUMN |
-                      DIAG_TILE_LAST | DIAG_NO_TILE_LAST | DIAG_FD_LDS | DIAG_COL_RADIX4 | DIAG_NO_IDENTITY |
-                      DIAG_NO_MID_DIRECT);
+    e->diag = flags & DIAG_ALL;
     return old;
 }
+// Deprecated process-wide form (the round-4 ABI): the flags every engine
+// created afterwards starts with.  Existing engines keep their own.
+static std::atomic<int> g_default_diag{0};
+extern "C" int rs16_set_diagnostics(int flags) { return g_default_diag.exchange(flags & DIAG_ALL); }
 extern "C" int rs16_prog_count(void) { return NUM_PROF; }
 extern "C" const char* rs16_prog_name(int prog) {
     static const char* names[] = {"GEN_FFT",   "GEN_IFFT",   "ENC_FIRST",     "ENC_MID",
@@ -224,7 +230,10 @@ static int resolve_rate(int rate, size_t k, size_t m, size_t S, bool* high, rs16
 static void detach(rs16_encoder* enc);
 static void detach(rs16_decoder* dec);
 
-extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
+extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) { return rs16_engine_new_ex(device, 0, err); }
+
+extern "C" rs16_engine* rs16_engine_new_ex(int device, int flags, rs16_error* err) {
+    if (flags & ~RS16_ENGINE_OWN_QUEUE) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
     int ndev = 0;
     hipError_t he = hipGetDeviceCount(&ndev);
     if (he != hipSuccess) return hip_fail(err, he), nullptr;
@@ -232,6 +241,7 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
     rs16_engine* e = new (std::nothrow) rs16_engine();
     if (!e) return set_error(err, RS16_INVALID_ARGUMENT), nullptr;
     e->device = device;
+    e->diag = g_default_diag.load();
     const HostTables& t = host_tables();
     auto fail = [&](hipError_t x) {
         hip_fail(err, x);
@@ -239,7 +249,20 @@ extern "C" rs16_engine* rs16_engine_new(int device, rs16_error* err) {
         return (rs16_engine*)nullptr;
     };
     if ((he = hipSetDevice(device)) != hipSuccess) return fail(he);
-    if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return fail(he);
+    if (flags & RS16_ENGINE_OWN_QUEUE) {
+        // A stream with a CU mask gets a hardware queue of its own (the HIP
+        // runtime shares its GPU_MAX_HW_QUEUES queues only among unmasked
+        // streams); the mask enables every CU.
+        int cus = 0;
+        if ((he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess) return fail(he);
+        std::vector<uint32_t> mask(((size_t)cus + 31) / 32, 0xFFFFFFFFu);
+        if (cus % 32) mask.back() = (1u << (cus % 32)) - 1;
+        if ((he = hipExtStreamCreateWithCUMask(&e->stream, (uint32_t)mask.size(), mask.data())) != hipSuccess)
+            return fail(he);
+    } else if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) {
+        return fail(he);
+    }
+    e->flags = flags;
     if ((he = hipMalloc(&e->d_skew_tab, (size_t)GF_ORDER * TAB_DWORDS * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_mul_tab, t.mul_tab.size() * 4)) != hipSuccess) return fail(he);
     if ((he = hipMalloc(&e->d_log_walsh, GF_ORDER * 2)) != hipSuccess) return fail(he);

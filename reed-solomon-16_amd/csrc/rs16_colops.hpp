@@ -58,14 +58,23 @@ __device__ __forceinline__ void glb_table(uint32_t (&t)[20], const uint32_t* tab
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef __attribute__((address_space(1))) const void* glb_vp;
 template <int NT>
-__device__ __forceinline__ void dma_copy(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
+__device__ __forceinline__ void dma_copy_step(const uint8_t* src, uint8_t* dst, uint32_t bytes, uint32_t i) {
     const uint32_t t = threadIdx.x, w = t >> 6;
+    const uint32_t c = i * NT + t;
+    if (c * 16 < bytes)
+        __builtin_amdgcn_global_load_lds((glb_vp)(src + c * 16), (lds_vp)(dst + (i * NT + 64 * w) * 16), 16, 0, 0);
+}
+// (sizes known at compile time: fully unrolled)
+template <int NT>
+__device__ __forceinline__ void dma_copy(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
 #pragma unroll
-    for (uint32_t i = 0; i * NT * 16 < bytes; i++) {
-        const uint32_t c = i * NT + t;
-        if (c * 16 < bytes)
-            __builtin_amdgcn_global_load_lds((glb_vp)(src + c * 16), (lds_vp)(dst + (i * NT + 64 * w) * 16), 16, 0, 0);
-    }
+    for (uint32_t i = 0; i * NT * 16 < bytes; i++) dma_copy_step<NT>(src, dst, bytes, i);
+}
+// (sizes known at run time only, e.g. mid_direct_kernel's nout x 2^hi
+// tables: a plain loop -- a full-unroll request cannot be honoured there)
+template <int NT>
+__device__ __forceinline__ void dma_copy_rt(const uint8_t* src, uint8_t* dst, uint32_t bytes) {
+    for (uint32_t i = 0; i * NT * 16 < bytes; i++) dma_copy_step<NT>(src, dst, bytes, i);
 }
 
 // Trade register bit RB (register pairs m, m | 2^RB) with lane bit LB of

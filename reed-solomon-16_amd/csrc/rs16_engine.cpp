@@ -449,6 +449,11 @@ int rs16_engine::decode_eval(const DecodeGeom& g, const uint8_t* flags_a, const 
     // (a prepared decode's outputs in ev_main are about to be overwritten)
     if (evset == &ev_main && !preparing)
         if (int rc = guard_eval(s, false, err)) return rc;
+    // Any evaluation other than the preparation itself also overwrites the
+    // path state below (e_ident, elog_fused, eval_in_col, var_ns) that a
+    // prepared decode reads -- whichever eval set it writes to (the
+    // pipelined host path's lanes use their own): the preparation is gone.
+    if (!preparing) prep.valid = false;
     const size_t nv = vary > 1 ? vary : 1;
     RS16_HIP(evset->work32.reserve(nv * VARY_WORK * 4));
     RS16_HIP(evset->elog.reserve(nv * VARY_WORK * 4));

@@ -71,6 +71,7 @@ struct rs16_decoder;
 
 struct rs16_engine {
     int device = 0;
+    int flags = 0;  // rs16_engine_new_ex flags (RS16_ENGINE_OWN_QUEUE)
     hipStream_t stream = nullptr;
     // diagnostic switches of this engine (rs16::DiagFlags, rs16_engine_set_diagnostics)
     int diag = 0;

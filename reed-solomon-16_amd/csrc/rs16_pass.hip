@@ -1858,7 +1858,7 @@ __global__ void __launch_bounds__(512) mid_direct_kernel(PassArgs a, const uint3
     };
     fetch(0, zl[0], zh[0]);
     uint4* tabs = (uint4*)mlds;
-    colops::dma_copy<W * 64>((const uint8_t*)(mtab + (size_t)nlo * N * 20), mlds, nout * N * 80);
+    colops::dma_copy_rt<W * 64>((const uint8_t*)(mtab + (size_t)nlo * N * 20), mlds, nout * N * 80);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();  // tables in LDS
     RS16_STAMP(a, 1);

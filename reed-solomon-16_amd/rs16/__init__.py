@@ -171,9 +171,11 @@ class Engine:
     device shard arrays (src/engine.rs:140-260).  Device arrays are passed as
     raw device pointers (int) or torch tensors."""
 
-    def __init__(self, device: int = 0):
+    OWN_QUEUE = 1  # RS16_ENGINE_OWN_QUEUE: the engine's stream on a hardware queue of its own
+
+    def __init__(self, device: int = 0, flags: int = 0):
         self._err = RS16Error()
-        self.h = lib().rs16_engine_new(device, C.byref(self._err))
+        self.h = lib().rs16_engine_new_ex(device, flags, C.byref(self._err))
         if not self.h:
             raise Error._from_c(self._err)
         self.device = device

@@ -35,6 +35,8 @@ SIGNATURES = {
     "rs16_engine_set_stamps": (_i, [_p, _p, _i, _e]),
     "rs16_engine_set_slices": (_i, [_p, _i, _e]),
     "rs16_engine_new": (_p, [_i, _e]),
+    "rs16_engine_new_ex": (_p, [_i, _i, _e]),
+    "rs16_set_diagnostics": (_i, [_i]),
     "rs16_engine_free": (None, [_p]),
     "rs16_engine_device": (_i, [_p]),
     "rs16_engine_stream": (_p, [_p]),

@@ -194,3 +194,19 @@ def test_column_slice_partition_matches_python():
             assert got == column_slices(S, n)
     with pytest.raises(rs16.Error):
         rs16.column_slice(100, 2, 0)
+
+
+def test_deprecated_process_diagnostics_default():
+    """rs16_set_diagnostics (the round-4 process-wide ABI, kept as a
+    deprecated wrapper): it sets the flags new engines start with
+    and returns the previous default; unknown bits are dropped.  No device
+    call is made."""
+    from rs16._lib import lib
+
+    L = lib()
+    prev = L.rs16_set_diagnostics(512 | (1 << 30))
+    try:
+        assert L.rs16_set_diagnostics(0) == 512
+        assert L.rs16_set_diagnostics(prev) == 0
+    finally:
+        L.rs16_set_diagnostics(prev)

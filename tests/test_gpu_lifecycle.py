@@ -139,3 +139,36 @@ def test_two_streams_share_engine_scratch():
     eng.destroy_stream(sa)
     eng.destroy_stream(sb_)
     eng.close()
+
+
+def test_engine_own_queue():
+    """rs16_engine_new_ex(RS16_ENGINE_OWN_QUEUE): the engine's stream has a
+    hardware queue of its own (a CU-masked stream).  Results are those of any
+    engine; two such engines run a stripe each at the same time; unknown
+    flags are refused."""
+    k = m = 4096
+    sb = 128
+    with pytest.raises(rs16.Error) as e:
+        rs16.Engine(0, 1 << 7)
+    assert e.value.kind == "InvalidArgument"
+    engs = [rs16.Engine(0, rs16.Engine.OWN_QUEUE), rs16.Engine(0, rs16.Engine.OWN_QUEUE)]
+    try:
+        data = []
+        for i, eng in enumerate(engs):
+            o = generate_original(k, sb, 40 + i)
+            d_o, d_r, d_x = DeviceArray.from_numpy(eng, o), DeviceArray(eng, m * sb), DeviceArray(eng, k * sb)
+            fo = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+            fr = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+            data.append((eng, o, d_o, d_r, d_x, fo, fr))
+        for _ in range(3):  # both engines' work in flight together
+            for eng, o, d_o, d_r, d_x, fo, fr in data:
+                rs16.encode_device(k, m, sb, d_o.ptr, d_r.ptr, engine=eng)
+                rs16.decode_device(k, m, sb, d_x.ptr, fo.ptr, d_r.ptr, fr.ptr, 0, m, engine=eng)
+        for eng, o, d_o, d_r, d_x, fo, fr in data:
+            eng.synchronize()
+            assert np.array_equal(d_r.download(shape=(m, sb)), O.encode(k, m, o))
+            assert np.array_equal(d_x.download(shape=(k, sb)), o)
+        del data
+    finally:
+        for eng in engs:
+            eng.close()

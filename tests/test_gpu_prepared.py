@@ -131,6 +131,41 @@ def test_prepared_rules(eng):
         eng.destroy_stream(side)
 
 
+def test_prepared_discarded_by_host_batch(eng):
+    """a pipelined host batch decode evaluates on its lanes' own
+    eval sets, but still rewrites the engine's path state (identity logs,
+    fused eval, column eval) a prepared decode reads.  A preparation followed
+    by a host batch decode is therefore discarded: the prepared call refuses
+    (InvalidArgument) instead of running the batch's path on logs that were
+    never written, and a fresh preparation restores bit for bit."""
+    k = m = 32768
+    sb = 64
+    original = generate_original(k, sb, 21)
+    recovery = O.encode(k, m, original)
+    d_r = DeviceArray.from_numpy(eng, recovery)
+    d_x = DeviceArray.from_numpy(eng, np.zeros_like(original))
+    # the preparation: every original lost (identity logs, no eval kernel)
+    d_fo = DeviceArray.from_numpy(eng, np.zeros(k, np.uint8))
+    d_fr = DeviceArray.from_numpy(eng, np.ones(m, np.uint8))
+    # the host batch: the reference bench's 1 % loss (general decode)
+    om, rm = masks(k, m, "1pct", 0)
+    h_o = np.stack([original, original])
+    h_o[:, ~om] = 0x3C
+    h_r = np.stack([recovery, recovery])
+    fo = np.ascontiguousarray(np.stack([om, om]).astype(np.uint8))
+    fr = np.ascontiguousarray(np.stack([rm, rm]).astype(np.uint8))
+    rs16.decode_prepare(k, m, sb, d_fo.ptr, d_fr.ptr, 0, m, engine=eng)
+    rs16.decode_host_batch(k, m, sb, 2, h_o, k * sb, fo, k, h_r, m * sb, fr, m, engine=eng)
+    for i in range(2):
+        assert np.array_equal(h_o[i], original), i
+    with pytest.raises(rs16.Error) as e:
+        rs16.decode_device_prepared(k, m, sb, d_x.ptr, d_r.ptr, engine=eng)
+    assert e.value.kind == "InvalidArgument"
+    rs16.decode_prepare(k, m, sb, d_fo.ptr, d_fr.ptr, 0, m, engine=eng)
+    rs16.decode_device_prepared(k, m, sb, d_x.ptr, d_r.ptr, engine=eng, check=True)
+    assert np.array_equal(d_x.download(shape=(k, sb)), original)
+
+
 def test_prepared_with_slices():
     e = rs16.Engine(0)
     try:
