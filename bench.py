@@ -493,6 +493,14 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
                     "engine B (encode_while_decode); not the metric"}
 
 
+def extra_on(name):
+    """Extras to leave out of a diagnostic run: RS16_BENCH_SKIP = comma list of
+    extra names (two_stripes, sustained, kib1000, batched, decode_1pct,
+    general_decodes, rate_paths, column_slices, configs4, host_resident,
+    host_batch, api_loop).  Unset for every real measurement."""
+    return name not in os.environ.get("RS16_BENCH_SKIP", "").split(",")
+
+
 def make_timed(sync, dist, world):
     """timed(fn, steps[, per_rank]): run fn `steps` times between two
     barriers (device sync + gloo barrier) and return the MAX over ranks of the
@@ -796,7 +804,7 @@ def main():
                   "decode_issue": "serial: rs16_decode_device" if args.split_decode else
                   "split: rs16_decode_prepare on a side stream during the encode, then rs16_decode_device_prepared"}
     two_early = None
-    if not args.no_extra and world == 1:
+    if not args.no_extra and world == 1 and extra_on("two_stripes"):
         # the serving-mode rate measured right here as well as after the
         # other extras: VERDICT r4 item 1 (probe 900 vs bench 756 GiB/s)
         two_early = two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, "right after the timed loop")
@@ -847,9 +855,9 @@ def main():
                         "the two-direction passes skip still count as butterflies here"}
 
     extra = {"serial_step" if args.split_decode else "split_decode_step": other_step}
-    if not args.no_extra:
+    if not args.no_extra and extra_on("sustained"):
         extra["sustained"] = sustained(eng, step, step_bytes * world, dist)
-    if not args.no_extra and (k, m) != (1000, 1000):
+    if not args.no_extra and (k, m) != (1000, 1000) and extra_on("kib1000"):
         # BASELINE configs[1] / [2]: 1000:1000 x 1 KiB encode, decode at 100 % loss
         k2 = m2 = 1000
         o2 = generate_original(k2, S, seed)
@@ -938,7 +946,7 @@ def main():
                     "decode_varied": "every stripe its own random loss of half its originals (general decode)"})
         extra["batched_stripes"] = bat
 
-    if not args.no_extra and loss >= 100:
+    if not args.no_extra and loss >= 100 and extra_on("decode_1pct"):
         # 1 % loss (benches/benchmarks.rs:84-87): originals 0..k-L and
         # recovery 0..L received, L = min(k, m) / 100; the last L originals
         # are restored in place.
@@ -961,10 +969,10 @@ def main():
                                      "decode_us": t1 / args.steps * 1e6, "lost_originals": L1,
                                      "received": f"originals 0..{k - L1}, recovery 0..{L1}"}
 
-    if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
+    if not args.no_extra and (k, m, S) == (32768, 32768, 1024) and extra_on("general_decodes"):
         extra["general_decodes"] = general_decodes(eng, k, m, S, original, d_rec, timed, args, world)
 
-    if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
+    if not args.no_extra and (k, m, S) == (32768, 32768, 1024) and extra_on("rate_paths"):
         # The multi-chunk rate paths: high rate with k > chunk
         # (60000:3000, 15 chunks of 4096) and low rate (3000:60000); encode,
         # then a decode that loses min(k, m) originals (the last ones for the
@@ -997,7 +1005,7 @@ def main():
                 "lost_originals": lost3}
         extra["rate_paths"] = rp
 
-    if not args.no_extra and world > 1 and S % (64 * world) == 0:
+    if not args.no_extra and world > 1 and S % (64 * world) == 0 and extra_on("column_slices"):
         # Strong scaling of ONE stripe (the 1 KiB configs over N
         # GPUs as S / N byte-column slices): every rank encodes and decodes its
         # column slice of the same 32768:32768 x 1 KiB stripe (here: slice r
@@ -1025,7 +1033,7 @@ def main():
             "gib_s": step_bytes * args.steps / ts / GIB, "ms_per_step": ts / args.steps * 1e3,
             "slice_bytes": w_s}
 
-    if not args.no_extra and (k, m, S) == (32768, 32768, 1024):
+    if not args.no_extra and (k, m, S) == (32768, 32768, 1024) and extra_on("configs4"):
         extra["configs4_rccl"] = configs4_rccl(eng, k, m, world, rank, dist, timed, barrier, args.steps)
 
     if two_early is not None:
@@ -1039,91 +1047,93 @@ def main():
         # slower).
         from rs16.device import PinnedArray
 
-        h_orig, h_rec, h_rest = PinnedArray(eng, k * S), PinnedArray(eng, m * S), PinnedArray(eng, k * S)
-        h_orig.array[:] = original.reshape(-1)
-        h_rest.array[:] = original.reshape(-1)
-        h_rest.array.reshape(k, S)[:loss] = 0
+        if extra_on("host_resident"):
+            h_orig, h_rec, h_rest = PinnedArray(eng, k * S), PinnedArray(eng, m * S), PinnedArray(eng, k * S)
+            h_orig.array[:] = original.reshape(-1)
+            h_rest.array[:] = original.reshape(-1)
+            h_rest.array.reshape(k, S)[:loss] = 0
 
-        def host_encode():
-            rs16.encode_host(k, m, S, h_orig.ptr, h_rec.ptr, engine=eng)
+            def host_encode():
+                rs16.encode_host(k, m, S, h_orig.ptr, h_rec.ptr, engine=eng)
 
-        def host_decode():
-            rs16.decode_host(k, m, S, h_rest.ptr, of, h_rec.ptr, rf, engine=eng)
+            def host_decode():
+                rs16.decode_host(k, m, S, h_rest.ptr, of, h_rec.ptr, rf, engine=eng)
 
-        host_encode()
-        host_decode()
-        assert np.array_equal(h_rec.array.reshape(m, S), recovery), "host-resident encode differs"
-        assert np.array_equal(h_rest.array.reshape(k, S), original), "host-resident decode did not restore"
-        n3 = max(3, args.steps // 4)
-        te, td = timed(host_encode, n3), timed(host_decode, n3)
-        extra["host_resident_pcie"] = {
-            "encode_gib_s": world * (k + m) * S * n3 / te / GIB, "decode_gib_s": world * (k + m) * S * n3 / td / GIB,
-            "encode_us": te / n3 * 1e6, "decode_us": td / n3 * 1e6,
-            "path": "pinned host buffers -> H2D -> device codec -> D2H (rs16_encode_host / rs16_decode_host)"}
-        del h_orig, h_rec, h_rest
-        # Several stripes, two in flight (rs16_encode_host_batch /
-        # rs16_decode_host_batch): stripe i + 1's H2D and stripe i - 1's D2H
-        # overlap stripe i's codec, so both link directions carry data.  Every
-        # stripe holds this stripe's data: each recovery must equal the one
-        # checked against the oracle fixture above, each decode restore it.
-        nb = 8
-        heng = eng
-        hb_o, hb_r = PinnedArray(heng, nb * k * S), PinnedArray(heng, nb * m * S)
-        hb_o.array.reshape(nb, k * S)[:] = original.reshape(1, -1)
-        fob = np.tile(of, nb)
-        frb = np.tile(rf, nb)
+            host_encode()
+            host_decode()
+            assert np.array_equal(h_rec.array.reshape(m, S), recovery), "host-resident encode differs"
+            assert np.array_equal(h_rest.array.reshape(k, S), original), "host-resident decode did not restore"
+            n3 = max(3, args.steps // 4)
+            te, td = timed(host_encode, n3), timed(host_decode, n3)
+            extra["host_resident_pcie"] = {
+                "encode_gib_s": world * (k + m) * S * n3 / te / GIB, "decode_gib_s": world * (k + m) * S * n3 / td / GIB,
+                "encode_us": te / n3 * 1e6, "decode_us": td / n3 * 1e6,
+                "path": "pinned host buffers -> H2D -> device codec -> D2H (rs16_encode_host / rs16_decode_host)"}
+            del h_orig, h_rec, h_rest
+        if extra_on("host_batch"):
+            # Several stripes, two in flight (rs16_encode_host_batch /
+            # rs16_decode_host_batch): stripe i + 1's H2D and stripe i - 1's D2H
+            # overlap stripe i's codec, so both link directions carry data.  Every
+            # stripe holds this stripe's data: each recovery must equal the one
+            # checked against the oracle fixture above, each decode restore it.
+            nb = 8
+            heng = eng
+            hb_o, hb_r = PinnedArray(heng, nb * k * S), PinnedArray(heng, nb * m * S)
+            hb_o.array.reshape(nb, k * S)[:] = original.reshape(1, -1)
+            fob = np.tile(of, nb)
+            frb = np.tile(rf, nb)
 
-        def batch_encode():
-            rs16.encode_host_batch(k, m, S, nb, hb_o.ptr, k * S, hb_r.ptr, m * S, engine=heng)
+            def batch_encode():
+                rs16.encode_host_batch(k, m, S, nb, hb_o.ptr, k * S, hb_r.ptr, m * S, engine=heng)
 
-        def batch_decode():
-            rs16.decode_host_batch(k, m, S, nb, hb_o.ptr, k * S, fob, k, hb_r.ptr, m * S, frb, m, engine=heng)
+            def batch_decode():
+                rs16.decode_host_batch(k, m, S, nb, hb_o.ptr, k * S, fob, k, hb_r.ptr, m * S, frb, m, engine=heng)
 
-        batch_encode()
-        assert all(np.array_equal(hb_r.array.reshape(nb, m, S)[i], recovery) for i in range(nb)), \
-            "pipelined host encode differs"
-        hb_o.array.reshape(nb, k, S)[:, :loss] = 0
-        batch_decode()
-        assert all(np.array_equal(hb_o.array.reshape(nb, k, S)[i], original) for i in range(nb)), \
-            "pipelined host decode did not restore"
-        # (the first calls after the buffers are created run at a fraction of
-        # the rate: scripts/probe_hostbatch.py reps 0-1; two more of each)
-        for _ in range(2):
             batch_encode()
+            assert all(np.array_equal(hb_r.array.reshape(nb, m, S)[i], recovery) for i in range(nb)), \
+                "pipelined host encode differs"
+            hb_o.array.reshape(nb, k, S)[:, :loss] = 0
             batch_decode()
-        n5 = max(4, args.steps // 4)
-        tbe = timed(batch_encode, n5)
-        tbd = timed(batch_decode, n5)
-        extra["host_batch_pipelined"] = {
-            "stripes_per_call": nb,
-            "encode_gib_s": world * nb * (k + m) * S * n5 / tbe / GIB,
-            "decode_gib_s": world * nb * (k + m) * S * n5 / tbd / GIB,
-            "encode_ms_per_call": tbe / n5 * 1e3, "decode_ms_per_call": tbd / n5 * 1e3,
-            "link_bytes_per_call": {"encode": nb * (k + m) * S, "decode_100pct": nb * (k + loss) * S},
-            "path": "pinned host stripes, two in flight: stripe i runs H2D -> codec -> D2H on lane i & 1 (a "
-                    "stream with buffers of its own), the lanes half a period apart so that one lane's D2H "
-                    "meets the other's H2D (rs16_encode_host_batch / rs16_decode_host_batch, DESIGN.md 3.10); "
-                    "every stripe's recovery == the fixture-checked one, every decode restored"}
-        del hb_o, hb_r
-        # The same calls in a fresh child process (scripts/probe_hostbatch.py,
-        # which checks every restored stripe): in this process, after the
-        # extras above, they run slower, and not for any cause found so far
-        # (NUMA node, streams created before the lanes, an RCCL communicator,
-        # the engine's state, GPU clocks after load: DESIGN.md 6.R5)
-        if world == 1:
-            res = subprocess.run([sys.executable, str(Path(__file__).resolve().parent / "scripts" / "probe_hostbatch.py"),
-                                  str(nb), "4"], capture_output=True, text=True, timeout=300)
-            last = [ln for ln in res.stdout.splitlines() if ln.startswith("rep 3: encode")]
-            if res.returncode == 0 and last and "restored True" in last[0]:
-                ln = last[0]
-                enc = float(ln.split("encode ")[1].split(" GiB/s")[0])
-                dec = float(ln.split("decode ")[1].split(" GiB/s")[0])
-                extra["host_batch_pipelined"]["fresh_process"] = {
-                    "encode_gib_s": enc, "decode_gib_s": dec,
-                    "note": "4th call of each in a child process (scripts/probe_hostbatch.py, 8 stripes, restored "
-                            "checked); the first calls of a process pay buffer setup"}
+            assert all(np.array_equal(hb_o.array.reshape(nb, k, S)[i], original) for i in range(nb)), \
+                "pipelined host decode did not restore"
+            # (the first calls after the buffers are created run at a fraction of
+            # the rate: scripts/probe_hostbatch.py reps 0-1; two more of each)
+            for _ in range(2):
+                batch_encode()
+                batch_decode()
+            n5 = max(4, args.steps // 4)
+            tbe = timed(batch_encode, n5)
+            tbd = timed(batch_decode, n5)
+            extra["host_batch_pipelined"] = {
+                "stripes_per_call": nb,
+                "encode_gib_s": world * nb * (k + m) * S * n5 / tbe / GIB,
+                "decode_gib_s": world * nb * (k + m) * S * n5 / tbd / GIB,
+                "encode_ms_per_call": tbe / n5 * 1e3, "decode_ms_per_call": tbd / n5 * 1e3,
+                "link_bytes_per_call": {"encode": nb * (k + m) * S, "decode_100pct": nb * (k + loss) * S},
+                "path": "pinned host stripes, two in flight: stripe i runs H2D -> codec -> D2H on lane i & 1 (a "
+                        "stream with buffers of its own), the lanes half a period apart so that one lane's D2H "
+                        "meets the other's H2D (rs16_encode_host_batch / rs16_decode_host_batch, DESIGN.md 3.10); "
+                        "every stripe's recovery == the fixture-checked one, every decode restored"}
+            del hb_o, hb_r
+            # The same calls in a fresh child process (scripts/probe_hostbatch.py,
+            # which checks every restored stripe): in this process, after the
+            # extras above, they run slower, and not for any cause found so far
+            # (NUMA node, streams created before the lanes, an RCCL communicator,
+            # the engine's state, GPU clocks after load: DESIGN.md 6.R5)
+            if world == 1:
+                res = subprocess.run([sys.executable, str(Path(__file__).resolve().parent / "scripts" / "probe_hostbatch.py"),
+                                      str(nb), "4"], capture_output=True, text=True, timeout=300)
+                last = [ln for ln in res.stdout.splitlines() if ln.startswith("rep 3: encode")]
+                if res.returncode == 0 and last and "restored True" in last[0]:
+                    ln = last[0]
+                    enc = float(ln.split("encode ")[1].split(" GiB/s")[0])
+                    dec = float(ln.split("decode ")[1].split(" GiB/s")[0])
+                    extra["host_batch_pipelined"]["fresh_process"] = {
+                        "encode_gib_s": enc, "decode_gib_s": dec,
+                        "note": "4th call of each in a child process (scripts/probe_hostbatch.py, 8 stripes, restored "
+                                "checked); the first calls of a process pay buffer setup"}
 
-    if not args.no_extra and world == 1:
+    if not args.no_extra and world == 1 and extra_on("api_loop"):
         # The reference's own API benchmark (ReedSolomonEncoder / Decoder with
         # per-shard add_* calls on host shards) through the C ABI.
         eng.synchronize()

@@ -160,7 +160,7 @@ extern "C" const char* rs16_prog_name(int prog) {
                                   "ENC_LAST",  "ENC_SINGLE", "DEC_FIRST",     "DEC_MID",
                                   "DEC_LAST",  "DEC_SINGLE", "DEC_HALF_LAST", "DEC_HALF_SINGLE",
                                   "DEC_HALF_FIRST", "DEC_HALF_MID", "EVAL_POLY", "COL_ENC", "COL_DEC",
-                                  "DEC_MID_DIRECT"};
+                                  "DEC_MID_DIRECT", "DEC_TILE_LAST"};
     static_assert(sizeof names / sizeof names[0] == NUM_PROF, "profiling names");
     return (prog >= 0 && prog < NUM_PROF) ? names[prog] : "?";
 }

@@ -816,17 +816,28 @@ int rs16_engine::decode_passes(const DecodeGeom& g, size_t S, size_t S_user, con
     a.in2 = U;
     a.out = nullptr;
     a.tile_base = t0;
-    // Few lost originals (lost-range pruning leaves a handful of tiles to
-    // this pass): one wave per quad column of each tile (tile_last_kernel)
-    // instead of one 8-wave item per 32 quads, whose latency was the pass.
+    // Lost originals in few tiles (lost-range pruning leaves a handful of
+    // tiles to this pass): one wave per quad column of each tile
+    // (tile_last_kernel) instead of one 8-wave item per 32 quads, whose
+    // latency was the pass.  Over more tiles the items win (scattered
+    // losses: 128 tiles 81 -> 37 us; break-even 16-32 tiles,
+    // scripts/probe_general.py).  How many tiles the lost originals span is
+    // known on the device only (lostrange): with <= 2048 lost both kernels
+    // are launched and each returns at once where the other one applies.
     const bool tile_last = lo == 8 && !(diag & DIAG_NO_TILE_LAST) && (lost <= 2048 || (diag & DIAG_TILE_LAST));
     if (tile_last) {
-        const uint32_t tiles = batch(t1 - t0, zs, zs, 0);
+        a.tl_max = (diag & DIAG_TILE_LAST) ? (1u << hi) : TILE_LAST_MAX;
+        // (the grid: tl_max tiles from the first lost original's, the kernel
+        // reads that tile from lostrange; a launch that returns at once costs
+        // per workgroup)
+        const uint32_t tiles = batch(std::min(t1 - t0, a.tl_max), zs, zs, 0);
         hipEvent_t ev;
         if (int rc = prof_begin(s, &ev, err)) return rc;
-        if (stamp_buf && stamp_prof == DEC_LAST) a.stamps = (uint64_t*)stamp_buf;
+        if (stamp_buf && stamp_prof == PROF_DEC_TILE_LAST) a.stamps = (uint64_t*)stamp_buf;
         RS16_HIP(launch_tile_last(a, tiles, s));
-        return prof_end(DEC_LAST, s, ev, err);
+        a.stamps = nullptr;
+        if (int rc = prof_end(PROF_DEC_TILE_LAST, s, ev, err)) return rc;
+        if (diag & DIAG_TILE_LAST) return RS16_OK;  // (every span is tile_last's)
     }
     RS16_PASS(DEC_LAST, lo, a, batch(t1 - t0, zs, zs, 0), s);
     return RS16_OK;

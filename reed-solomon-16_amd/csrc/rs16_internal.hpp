@@ -91,6 +91,7 @@ enum ProfId : int {
     PROF_COL_ENC,  // one-launch codec (rs16_col.hip): encode
     PROF_COL_DEC,  // one-launch codec: half-transform decode
     PROF_DEC_MID_DIRECT,  // the general decode's middle pass as a direct product (mid_direct_kernel)
+    PROF_DEC_TILE_LAST,   // the general decode's last pass, one wave per quad column (tile_last_kernel)
     NUM_PROF
 };
 
@@ -198,6 +199,12 @@ struct PassArgs {
     // the consumed tile rows (from lostrange) are at most mid_direct; those
     // DEC_MID workgroups return at once (0: no direct kernel)
     uint32_t mid_direct;
+    // DEC_LAST at 2^8-row tiles: when tl_max > 0 the lost originals' tiles
+    // (lostrange) are the last pass of tile_last_kernel if they span at most
+    // tl_max tiles, else of the 8-wave DEC_LAST items; each launch checks on
+    // the device and returns at once when the other one covers the stripe
+    // (0: DEC_LAST alone, no tile_last_kernel launch)
+    uint32_t tl_max;
 };
 
 // One-launch codec for 2^9 / 2^10-row transforms (rs16_col.hip): one
@@ -303,6 +310,10 @@ hipError_t launch_tile_last(const PassArgs& a, uint32_t num_tiles, hipStream_t s
 // stripes; a stripe whose consumed rows exceed MID_DIRECT_MAX does nothing
 // (DEC_MID computes it).
 constexpr uint32_t MID_DIRECT_MAX = 4;
+// tile_last_kernel is the general decode's last pass when the lost originals
+// span at most this many 256-row tiles (scripts/probe_general.py: 16 tiles
+// 18.6 against 24.0 us for the 8-wave items, 32 tiles 28.3 against 24.7)
+constexpr uint32_t TILE_LAST_MAX = 16;
 hipError_t launch_mid_direct(const PassArgs& a, const uint32_t* mtab, uint32_t hi, uint32_t ns, hipStream_t s);
 
 // Elementwise / small kernels.

@@ -211,6 +211,13 @@ __device__ __forceinline__ bool row_below(uint32_t ur, uint32_t lr, uint32_t lim
     return ur < lim && lr < lim - ur;
 }
 
+// The last pass's lost-original tiles (2^T rows each) span at most tl_max
+// tiles: tile_last_kernel is the last pass of the stripe (else DEC_LAST).
+template <int T> __device__ __forceinline__ bool tl_covers(const PassArgs& a) {
+    const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
+    return r0 < r1 && ((r1 - 1) >> T) - (r0 >> T) < a.tl_max;
+}
+
 // The consumed U rows [nlo, nhi) of the general decode's middle pass, when
 // at most MID_DIRECT_MAX (mid_direct_kernel: the direct product).
 __device__ __forceinline__ bool mid_need(const PassArgs& a, uint32_t& nlo, uint32_t& nhi) {
@@ -1557,6 +1564,8 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
         if (a.lostrange) {
             const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
             if (!((tile << T) < r1 && ((tile + 1) << T) > r0)) return;
+            // (tile_last_kernel took this stripe's few tiles)
+            if (a.tl_max && tl_covers<T>(a)) return;
         }
     }
     // one item per workgroup (launch_pass sets per_wg = 1): straight-line code
@@ -1643,11 +1652,18 @@ __global__ void __launch_bounds__(256) tile_last_kernel(PassArgs a) {
         if (a.zflags) a.zflags += st * a.bs_zflags;
         if (a.lostrange) a.lostrange += st * a.bs_lost;
     }
-    tile += a.tile_base;
     if (a.lostrange) {
-        // a tile without a lost original stores nothing
+        // The grid covers min(tiles, tl_max) tiles per stripe, counted from
+        // the first one with a lost original; lost originals over more than
+        // tl_max tiles are DEC_LAST's (its 8-wave items win there:
+        // scripts/probe_general.py, break-even 16-32 tiles), and a tile past
+        // the last lost original stores nothing.
         const uint32_t r0 = ((cu32p)a.lostrange)[0], r1 = ((cu32p)a.lostrange)[1];
-        if (!((tile << T) < r1 && ((tile + 1) << T) > r0)) return;
+        if (!tl_covers<T>(a)) return;
+        tile += r0 >> T;
+        if (tile > ((r1 - 1) >> T)) return;
+    } else {
+        tile += a.tile_base;
     }
     RS16_STAMP(a, 0);
     const uint32_t q = qg * 4 + w;

@@ -19,6 +19,8 @@
 #   stamps=PROGS[+K]      phase timeline of pass programs PROGS (comma list) at k = m = K (default
 #                         32768) with the stamps build (make -C reed-solomon-16_amd/csrc stamps:
 #                         reed-solomon-16_amd/build_stamps/librs16.so) -> stamps_N.json
+#   ab=DIRA,DIRB[+REPS[+ARGS]]  same-box A/B: bench.py --no-extra --no-cpu-baseline ARGS with
+#                         RS16_LIB=reed-solomon-16_amd/DIRA/librs16.so, then DIRB, alternating, REPS (3) times
 #   slices                bench.py at 1 / 2 / 4 column slices, fresh process per run, 3 reps
 #                         (the profiles/r05_slices.txt measurement)
 #
@@ -81,6 +83,20 @@ for step in "$@"; do
       RS16_LIB=reed-solomon-16_amd/build_stamps/librs16.so RS16_STAMP_PROGS=$progs RS16_STAMPS_OUT=$TAG/stamps_$n.json \
           timeout -k 10 300 python scripts/stamps.py $size > "$O/stamps_$n.txt" 2>&1 || fail stamps "$O/stamps_$n.txt"
       cut -c1-1500 "$O/stamps_$n.txt" ;;
+    ab)
+      dirs=${arg%%+*}
+      rest=""
+      [ "$dirs" != "$arg" ] && rest=${arg#*+}
+      reps=${rest%%+*}
+      bargs=""
+      [ "$reps" != "$rest" ] && bargs=${rest#*+}
+      for rep in $(seq 1 ${reps:-3}); do
+        for d in ${dirs//,/ }; do
+          RS16_LIB=reed-solomon-16_amd/$d/librs16.so timeout -k 10 200 python bench.py --no-extra --no-cpu-baseline \
+              ${bargs//+/ } > "$O/ab_${d}_$rep.json" 2> "$O/ab.err" || fail ab "$O/ab.err"
+          echo "$d rep=$rep $(python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(d['value'], d['ms_per_step'], d['kernels_us'])" "$O/ab_${d}_$rep.json")"
+        done
+      done ;;
     slices)
       for rep in 1 2 3; do
         for sl in 1 2 4; do

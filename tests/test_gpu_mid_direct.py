@@ -188,3 +188,53 @@ def test_slices(eng):
         run(eng, k, m, sb, om, rm, 0, 9)
     finally:
         eng.set_slices(1)
+
+
+def masks_span(k, m, span_tiles, nlost, seed, tr=256):
+    """nlost originals lost, scattered over the last `span_tiles` 256-row
+    tiles of the originals (first and last of them lost); as many random
+    recovery shards received."""
+    rng = np.random.default_rng(seed)
+    lo = max(0, k - span_tiles * tr)
+    om = np.ones(k, bool)
+    om[rng.choice(np.arange(lo, k), min(nlost, k - lo), replace=False)] = False
+    om[lo] = om[k - 1] = False
+    rm = np.zeros(m, bool)
+    rm[rng.choice(m, int((~om).sum()), replace=False)] = True
+    return om, rm
+
+
+@pytest.mark.parametrize("diag", [0, rs16.DIAG_TILE_LAST, rs16.DIAG_NO_TILE_LAST], ids=["auto", "tile_last", "items"])
+@pytest.mark.parametrize("span", [1, 15, 16, 17, 40, 128])
+def test_last_pass_choice_by_span(eng, span, diag):
+    """The general decode's last pass at 2^16 work rows: tile_last_kernel for
+    lost originals spanning <= TILE_LAST_MAX = 16 tiles, the 8-wave DEC_LAST
+    items beyond (decided on the device from the lost range: both launch,
+    each returns where the other applies).  Scattered losses over 1..128
+    tiles, each form forced as the control."""
+    k = m = 32768
+    om, rm = masks_span(k, m, span, 300, span)
+    run(eng, k, m, 128, om, rm, diag, span)
+
+
+def test_last_pass_choice_batched_varied(eng):
+    """Stripes of one call whose lost ranges fall on either side of the cut
+    (the kernels decide per stripe)."""
+    k = m = 32768
+    sb, ns = 64, 3
+    spans = [2, 40, 16]
+    origs = [generate_original(k, sb, 50 + i) for i in range(ns)]
+    recs = [O.encode(k, m, o) for o in origs]
+    oms, rms = zip(*[masks_span(k, m, s, 200, 60 + i) for i, s in enumerate(spans)])
+    held = np.stack(origs)
+    for i in range(ns):
+        held[i][~oms[i]] = 0x5C
+    d_x = DeviceArray.from_numpy(eng, held.reshape(-1))
+    d_r = DeviceArray.from_numpy(eng, np.stack(recs).reshape(-1))
+    d_fo = DeviceArray.from_numpy(eng, np.stack(oms).astype(np.uint8).reshape(-1))
+    d_fr = DeviceArray.from_numpy(eng, np.stack(rms).astype(np.uint8).reshape(-1))
+    rs16.decode_device_batch_varied(k, m, sb, ns, d_x.ptr, k * sb, d_fo.ptr, k, d_r.ptr, m * sb, d_fr.ptr, m,
+                                    [int(o.sum()) for o in oms], [int(r.sum()) for r in rms], engine=eng)
+    back = d_x.download(shape=(ns, k, sb))
+    for i in range(ns):
+        assert np.array_equal(back[i], origs[i]), spans[i]
