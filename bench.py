@@ -440,7 +440,10 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
         encode()
         decode()
 
-    t1 = run([eng], one, 10, 3) / 10
+    # steady state: 30 untimed iterations, then 200 timed (a 20-step loop
+    # right after a sync includes the GPU's clock ramp; scripts/probe_own_queue.py)
+    nst, nwu = max(200, args.steps), 30
+    t1 = run([eng], one, nst, nwu) / nst
 
     def pair(flags):
         eng2 = rs16.Engine(local, flags)
@@ -468,8 +471,8 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
         two()
         eng2.synchronize()
         assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
-        t2 = run([eng, eng2], two, args.steps, args.warmup)
-        t3 = run([eng, eng2], enc_dec, args.steps, args.warmup)
+        t2 = run([eng, eng2], two, nst, nwu)
+        t3 = run([eng, eng2], enc_dec, nst, nwu)
         assert np.array_equal(x2.download(shape=(k, S)), o2), "second stream: decode did not restore"
         del a2, r2, x2, f2o, f2r
         eng2.close()
@@ -477,15 +480,15 @@ def two_stripes(eng, local, k, m, S, of, rf, loss, encode, decode, args, where):
 
     t2, t3 = pair(rs16.Engine.OWN_QUEUE)
     t2d, t3d = pair(0)
-    return {"gib_s": 2 * step_bytes * args.steps / t2 / GIB, "ms_per_two_stripes": t2 / args.steps * 1e3,
-            "encode_while_decode_gib_s": step_bytes * args.steps / t3 / GIB,
-            "encode_while_decode_us": t3 / args.steps * 1e6, "where": where,
+    return {"gib_s": 2 * step_bytes * nst / t2 / GIB, "ms_per_two_stripes": t2 / nst * 1e3,
+            "encode_while_decode_gib_s": step_bytes * nst / t3 / GIB,
+            "encode_while_decode_us": t3 / nst * 1e6, "where": where, "steps": nst, "warmup": nwu,
             "one_stripe_gib_s": step_bytes / t1 / GIB,
-            "two_stripe_time_over_one": round(t2 / args.steps / t1, 3),
+            "two_stripe_time_over_one": round(t2 / nst / t1, 3),
             "second_engine": "rs16_engine_new_ex(RS16_ENGINE_OWN_QUEUE): one engine, no selection",
-            "default_second_engine": {"gib_s": 2 * step_bytes * args.steps / t2d / GIB,
-                                      "encode_while_decode_gib_s": step_bytes * args.steps / t3d / GIB,
-                                      "two_stripe_time_over_one": round(t2d / args.steps / t1, 3),
+            "default_second_engine": {"gib_s": 2 * step_bytes * nst / t2d / GIB,
+                                      "encode_while_decode_gib_s": step_bytes * nst / t3d / GIB,
+                                      "two_stripe_time_over_one": round(t2d / nst / t1, 3),
                                       "note": "second engine from rs16_engine_new: its stream's hardware queue is "
                                               "the runtime's choice (a shared queue runs the pair serially, ~2.0)"},
             "note": "serving-mode throughput: two independent 32768:32768 x 1 KiB stripes in flight "
@@ -767,7 +770,7 @@ def main():
     # steps and the timed loop, so that the timed loop runs unprofiled and
     # in the state the profiled copy leaves the GPU in (a GPU coming out of
     # idle runs steps ~10-25 of a cold start ~8 % slower while its clocks
-    # settle: extra.sustained).  Its own first 40 steps warm
+    # settle: extra.sustained, CHANGELOG.md round 4).  Its own first 40 steps warm
     # the clocks and are not counted.  One column slice, so that every
     # timed launch is one kernel running alone.
     # The events are read (host work, GPU idle) only after the timed loop.
@@ -1044,7 +1047,7 @@ def main():
         # the device-resident rate): rs16_encode_host / rs16_decode_host on
         # pinned buffers = H2D of the inputs, the same device codec, D2H of
         # the outputs (whole-width slices: narrower pipelined slices measured
-        # slower).
+        # slower, CHANGELOG.md round 1).
         from rs16.device import PinnedArray
 
         if extra_on("host_resident"):
@@ -1119,7 +1122,7 @@ def main():
             # which checks every restored stripe): in this process, after the
             # extras above, they run slower, and not for any cause found so far
             # (NUMA node, streams created before the lanes, an RCCL communicator,
-            # the engine's state, GPU clocks after load: DESIGN.md 6.R5)
+            # the engine's state, GPU clocks after load: CHANGELOG.md round 5)
             if world == 1:
                 res = subprocess.run([sys.executable, str(Path(__file__).resolve().parent / "scripts" / "probe_hostbatch.py"),
                                       str(nb), "4"], capture_output=True, text=True, timeout=300)

@@ -17,7 +17,7 @@
 // the all-zero v_perm table (skew_tab, rs16_tables.cpp).
 //
 // Why one launch: at 1000:1000 x 1 KiB the three-pass codec is a chain of
-// latency-bound kernels of 128-256 one-wave workgroups.  Here
+// latency-bound kernels of 128-256 one-wave workgroups (CHANGELOG.md round 3).  Here
 // every quad column (8 bytes of each row: 4 elements, an independent set of
 // codewords, src/algorithm.md:18-32) is one workgroup that keeps the whole
 // column -- 2^L rows x 8 bytes, 8 KiB at L = 10 -- resident for all 2L layers:
@@ -726,7 +726,7 @@ __global__ __launch_bounds__((1 << L) / 4) void col_kernel(ColArgs a) {
 // (col2_kernel): 2 rows per thread, 2^(L-1) threads -- 8 waves at L = 10, two
 // per SIMD -- instead of 4 rows in 2^(L-2) threads.  The codec's time at
 // 1000:1000 x 1 KiB is the dependency chain of one wave (one per SIMD, 128
-// workgroups on 256 CUs): halving a lane's rows halves the
+// workgroups on 256 CUs, CHANGELOG.md round 4): halving a lane's rows halves the
 // chain, and the second wave of each SIMD issues into the first one's
 // stalls, at the price of one in-wave row-bit swap per layer instead of per
 // two.  A layer's butterfly pairs the thread's two rows (register bit RB);

@@ -401,7 +401,7 @@ int rs16_engine::encode_high_fused(size_t k, size_t m, size_t S, size_t S_user, 
         return RS16_OK;
     }
     // odd L: the extra row bit goes to the strided two-direction pass (an
-    // 8 / 7 / 8 split measured 2-3 us slower per encode)
+    // 8 / 7 / 8 split measured 2-3 us slower per encode, CHANGELOG.md round 3)
     const int lo = L / 2, hi = L - lo;
     const size_t zs = chunk * S;
     a.out = Z;

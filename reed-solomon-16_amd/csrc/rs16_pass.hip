@@ -17,7 +17,7 @@
 //   One item per workgroup: the twiddle tables of the tile are requested
 //   first and the tile's rows right behind them, then staged, computed and
 //   stored (a software-pipelined persistent variant
-//   measured slower at every T).
+//   measured slower at every T, CHANGELOG.md round 3).
 //
 //   Lane = quad.  Each thread keeps 16 rows ("a row set") of its quad in
 //   VGPRs (8 at T = 5); a wave holds 64/Q row sets (Q = 32 quads per tile row
@@ -73,7 +73,7 @@ enum LoadMode { LD_PLAIN = 0, LD_GATHER_ENC, LD_GATHER_DEC, LD_DEC_LAST };
 enum StoreMode { ST_PLAIN = 0, ST_RECOVERY, ST_RESTORE };
 
 // Store cache policy: non-temporal stores in the single-direction passes,
-// plain stores in the two-direction passes (same-box A/B, DESIGN.md 6.1:
+// plain stores in the two-direction passes (same-box A/B, CHANGELOG.md round 3:
 // nt / sc1 / sc0 sc1 everywhere and nt loads all measured slower).
 template <int P> struct ProgTraits;
 #define RS16_PROG(P, LD, I, F, FF, ST)          \

@@ -102,6 +102,52 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(copy2, dim3(2 * blocks), dim3(256), 0, s0, (const u32x4*)h_in, (u32x4*)d_a,
                            (const u32x4*)d_b, (u32x4*)h_out, n16, blocks);
     });
+    // a copy engine one way, a copy kernel the other way (no two copy-engine
+    // jobs that could be queued on one engine)
+    time("memcpy H2D + kernel D2H", 2, [&] {
+        hipEvent_t f;
+        CK(hipEventCreateWithFlags(&f, hipEventDisableTiming));
+        CK(hipEventRecord(f, s0));
+        CK(hipStreamWaitEvent(s1, f, 0));
+        CK(hipEventDestroy(f));
+        CK(hipMemcpyAsync(d_a, h_in, bytes, hipMemcpyHostToDevice, s0));
+        hipLaunchKernelGGL(copy2, dim3(blocks), dim3(256), 0, s1, (const u32x4*)d_b, (u32x4*)h_out,
+                           (const u32x4*)d_b, (u32x4*)h_out, n16, blocks);
+        hipEvent_t j;
+        CK(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+        CK(hipEventRecord(j, s1));
+        CK(hipStreamWaitEvent(s0, j, 0));
+        CK(hipEventDestroy(j));
+    });
+    // H2D on stream a, D2H on stream b, for pairs of 4 streams: which pairs
+    // overlap (copy engines per stream are the runtime's choice)
+    hipStream_t ss[4];
+    for (auto& x : ss) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (int a = 0; a < 4; a++)
+        for (int b = 0; b < 4; b++) {
+            if (a == b) continue;
+            char name[64];
+            snprintf(name, sizeof name, "memcpy H2D s%d + D2H s%d", a, b);
+            time(name, 2, [&] {
+                hipEvent_t f;
+                CK(hipEventCreateWithFlags(&f, hipEventDisableTiming));
+                CK(hipEventRecord(f, s0));
+                CK(hipStreamWaitEvent(ss[a], f, 0));
+                CK(hipStreamWaitEvent(ss[b], f, 0));
+                CK(hipEventDestroy(f));
+                CK(hipMemcpyAsync(d_a, h_in, bytes, hipMemcpyHostToDevice, ss[a]));
+                CK(hipMemcpyAsync(h_out, d_b, bytes, hipMemcpyDeviceToHost, ss[b]));
+                hipEvent_t j0, j1;
+                CK(hipEventCreateWithFlags(&j0, hipEventDisableTiming));
+                CK(hipEventCreateWithFlags(&j1, hipEventDisableTiming));
+                CK(hipEventRecord(j0, ss[a]));
+                CK(hipEventRecord(j1, ss[b]));
+                CK(hipStreamWaitEvent(s0, j0, 0));
+                CK(hipStreamWaitEvent(s0, j1, 0));
+                CK(hipEventDestroy(j0));
+                CK(hipEventDestroy(j1));
+            });
+        }
     // check the last copies
     unsigned char* ha = (unsigned char*)malloc(bytes);
     CK(hipMemcpy(ha, d_a, bytes, hipMemcpyDeviceToHost));
