@@ -99,6 +99,15 @@ RS16_PROG(DEC_HALF_LAST, LD_PLAIN, false, false, true, ST_RESTORE)
 RS16_PROG(DEC_HALF_SINGLE, LD_GATHER_DEC, true, false, true, ST_RESTORE)
 #undef RS16_PROG
 
+// Quads per tile row of the T = 7 passes (the encoder's first / last
+// passes and the identity decode's): 64 -- 8-wave workgroups, two per CU,
+// 512 items for a 32768-row stripe, each twiddle table staged once per 64
+// quad columns -- against 32 (4-wave workgroups, four per CU, 1024 items):
+// same-box A/B x 8, 805-815 -> 797-838 GiB/s, mean +1.5 %, 6 of 8 pairs
+// faster (profiles/r06_t7_q64_ab.txt).  (-DRS16_T7_Q=32: the old geometry.)
+#ifndef RS16_T7_Q
+#define RS16_T7_Q 64
+#endif
 // Row bits in registers: 4 (16 rows per thread) from T = 6 on; 3 at T = 5
 // (the passes of the n <= 2048 codecs, which are latency-bound: 8 rows per
 // thread and 16 quads per tile row give twice the waves, each with half the
@@ -110,7 +119,7 @@ template <int T> struct Geo {
     static constexpr int SETS = 1 << (T - R);             // row sets per tile
     // quads per tile row: 32 (two 16-row sets per wave) from T = 6 on, 16
     // (four 8-row sets per wave) at T = 5, 64 (one row set) below
-    static constexpr int Q = T > 4 ? (R == 3 ? 16 : 32) : 64;
+    static constexpr int Q = T > 4 ? (R == 3 ? 16 : (T == 7 ? RS16_T7_Q : 32)) : 64;
     static constexpr int HWS = 64 / Q;                    // row sets per wave
     static constexpr int W = SETS / HWS > 0 ? SETS / HWS : 1;  // waves per workgroup
     static constexpr int SHB = T - R;                     // layout B: k = s + (m << SHB)

@@ -10,6 +10,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #define CK(x)                                                                       \
     do {                                                                            \
@@ -51,6 +54,14 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_b, bytes));
     memset(h_in, 1, bytes);
     memset(h_out, 2, bytes);
+    {
+        // where this process runs and where its pinned pages live (NUMA node of
+        // the first page of each buffer, move_pages with no target = query)
+        void* pages[2] = {h_in, h_out};
+        int status[2] = {-1, -1};
+        const long rc = syscall(SYS_move_pages, 0, 2, pages, nullptr, status, 0);
+        printf("cpu %d, pinned pages on NUMA nodes %d / %d (move_pages rc %ld)\n", sched_getcpu(), status[0], status[1], rc);
+    }
     CK(hipMemset(d_a, 3, bytes));
     CK(hipMemset(d_b, 4, bytes));
     hipStream_t s0, s1;
