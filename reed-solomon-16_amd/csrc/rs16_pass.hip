@@ -129,10 +129,18 @@ template <int T> struct Geo {
     static constexpr int TSPLIT = T > 4 ? (1 << T) - (1 << (T - R)) : 0;
 };
 
-// The layout switch goes through the LDS image in one round (32 KiB at
-// T = 6..8: 2^T rows x Q quads x 8 bytes).
+template <int P, int T, int QL> struct SmemL;
+// The layout switch goes through an LDS image of 2^T rows x QL quads x 8
+// bytes, in Q / QL rounds.  One round (4 barriers -> 2 per switch, every
+// LDS instruction with all lanes) when the program's whole layout still lets
+// two workgroups share a CU (<= 80 KiB: the T = 7 encode passes, 64-quad
+// rows); else two rounds of Q / 2 quads (the T = 8 passes, the decoders' T =
+// 7 passes with their multiplier tables).
+#ifndef RS16_ONE_ROUND_MAX
+#define RS16_ONE_ROUND_MAX (80 * 1024)
+#endif
 template <int P, int T> struct Rnd {
-    static constexpr int NQR = T >= 7 ? 2 : 1;
+    static constexpr int NQR = T >= 7 && SmemL<P, T, Geo<T>::Q>::BYTES > RS16_ONE_ROUND_MAX ? 2 : 1;
     static constexpr int QL = Geo<T>::Q / NQR;
 };
 
@@ -144,10 +152,10 @@ template <int P, int T> struct Rnd {
 // Everything but the image is per tile key and stays resident across the
 // items of that key.  At T = 8 the largest program (DEC_LAST) needs 75 KiB,
 // so two workgroups share a CU.
-template <int P, int T> struct Smem {
+template <int P, int T, int QL> struct SmemL {
     using PT = ProgTraits<P>;
     static constexpr bool TWO = PT::IFFT && PT::FFT;
-    static constexpr int IMG_BYTES = T > 4 ? (1 << T) * Rnd<P, T>::QL * 8 : 0;
+    static constexpr int IMG_BYTES = T > 4 ? (1 << T) * QL * 8 : 0;
     static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
     static constexpr int ERT_OFF = IMG_BYTES;
     static constexpr int TAB1_BYTES = Geo<T>::NTAB * 80;
@@ -167,6 +175,7 @@ template <int P, int T> struct Smem {
     static constexpr int ELOG_OFF = LOST_OFF + LOST_BYTES;
     static constexpr int BYTES = ELOG_OFF + ELOG_BYTES;
 };
+template <int P, int T> struct Smem : SmemL<P, T, Rnd<P, T>::QL> {};
 
 struct Thr {
     uint32_t lane, w, s;   // lane, wave, row set
