@@ -139,6 +139,13 @@ template <int P, int T, int QL> struct SmemL;
 #ifndef RS16_ONE_ROUND_MAX
 #define RS16_ONE_ROUND_MAX (80 * 1024)
 #endif
+// The encoder's two-direction pass at T = 8 (ENC_MID, also the identity
+// decode's middle pass): its one-round image (64 KiB) shares its LDS with
+// the layout-A twiddle tables, which are dead during both layout switches
+// (-DRS16_MID_SHARED=0: two rounds, tables beside the image).
+#ifndef RS16_MID_SHARED
+#define RS16_MID_SHARED 1
+#endif
 template <int P, int T> struct Rnd {
     static constexpr int NQR = T >= 7 && SmemL<P, T, Geo<T>::Q>::BYTES > RS16_ONE_ROUND_MAX ? 2 : 1;
     static constexpr int QL = Geo<T>::Q / NQR;
@@ -156,9 +163,14 @@ template <int P, int T, int QL> struct SmemL {
     using PT = ProgTraits<P>;
     static constexpr bool TWO = PT::IFFT && PT::FFT;
     static constexpr int IMG_BYTES = T > 4 ? (1 << T) * QL * 8 : 0;
+    // SHARED (ENC_MID at T = 8, one round): [image 64 KiB, holding the
+    // layout-A tables of each direction outside the switches][IFFT layout-B
+    // tables][FFT layout-B tables]
+    static constexpr bool SHARED = RS16_MID_SHARED && P == ENC_MID && T == 8 && QL == Geo<T>::Q;
     static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
     static constexpr int ERT_OFF = IMG_BYTES;
-    static constexpr int TAB1_BYTES = Geo<T>::NTAB * 80;
+    static constexpr int TABB_OFF = IMG_BYTES;  // (SHARED: the IFFT's layout-B tables)
+    static constexpr int TAB1_BYTES = SHARED ? 0 : Geo<T>::NTAB * 80;
     // Restage (one-item build, T > 4): tab2 holds only the second
     // direction's layout-B tables; its layout-A tables are written over the
     // first direction's in tab1 at the first layout switch.
@@ -166,8 +178,8 @@ template <int P, int T, int QL> struct SmemL {
     static constexpr int TAB2_BYTES = TWO ? (RESTAGE ? Geo<T>::NTAB - Geo<T>::TSPLIT : Geo<T>::NTAB) * 80 : 0;
     static constexpr int RVT_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 80 : 0;
     static constexpr int LOST_BYTES = PT::STORE == ST_RESTORE ? (1 << T) * 4 : 0;
-    static constexpr int TAB1_OFF = ERT_OFF + ERT_BYTES;
-    static constexpr int TAB2_OFF = TAB1_OFF + TAB1_BYTES;
+    static constexpr int TAB1_OFF = SHARED ? 0 : ERT_OFF + ERT_BYTES;
+    static constexpr int TAB2_OFF = SHARED ? TABB_OFF + (Geo<T>::NTAB - Geo<T>::TSPLIT) * 80 : TAB1_OFF + TAB1_BYTES;
     static constexpr int RVT_OFF = TAB2_OFF + TAB2_BYTES;
     static constexpr int LOST_OFF = RVT_OFF + RVT_BYTES;
     // erasure logs of the tile's rows when the pass finishes eval_poly (ework)
@@ -1037,7 +1049,12 @@ template <int P, int T> struct TileStage {
     // second direction at the start: all of it, or only its layout-B tables
     static constexpr int N2 = !SM::TWO ? 0 : (LateS2<P, T>::value ? G::NTAB - G::TSPLIT : G::NTAB);
     static constexpr bool S2 = N2 > 0;
-    Stager<T, G::NTAB> s1;
+    // (SHARED: the first direction's layout-A tables into the image region,
+    // its layout-B tables beside it)
+    static constexpr int N1 = SM::SHARED ? G::TSPLIT : G::NTAB;
+    static constexpr int N1B = SM::SHARED ? G::NTAB - G::TSPLIT : 0;
+    Stager<T, N1> s1;
+    Stager<T, N1B> s1b;
     Stager<T, N2> s2;
 
     uint32_t ev[4];  // wave 0: the tile's 256-row block of eval_poly's work (ework)
@@ -1072,6 +1089,7 @@ template <int P, int T> struct TileStage {
             }
         }
         s1.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, PT::IFFT ? a.skew_ifft : a.skew_fft});
+        if constexpr (N1B > 0) s1b.issue(a.skew_tab, TwiddleEntry<T>{a, c, G::TSPLIT, a.skew_ifft});
         if constexpr (S2) s2.issue(a.skew_tab, TwiddleEntry<T>{a, c, G::NTAB - N2, a.skew_fft});
     }
     // Decoder gather staging, run before the tile's row loads: the erasure
@@ -1126,6 +1144,7 @@ template <int P, int T> struct TileStage {
         }
         if constexpr (S2) s2.commit((uint4*)(smem + SM::TAB2_OFF));
         s1.commit((uint4*)(smem + SM::TAB1_OFF));
+        if constexpr (N1B > 0) s1b.commit((uint4*)(smem + SM::TABB_OFF));
         __syncthreads();  // staged tables visible
     }
 };
@@ -1376,6 +1395,9 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         if (!d.ztile) tile_fd<T, NQR, START_B>(L, H, d.zl, d.zh, c, lds);
     }
 
+    // SHARED: the second direction's layout-A tables are requested after the
+    // first layout switch and written over the image after the second
+    [[maybe_unused]] Stager<T, (SM::SHARED ? G::TSPLIT : 0)> s3s;
     // ---------------- IFFT ----------------
     bool in_b = START_B;
     if constexpr (PT::IFFT) {
@@ -1386,12 +1408,16 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         RS16_STAMP(a, 3);
         prio<P, 1, T>();
         if constexpr (T > 4) {
-            Stager<T, (LateS2<P, T>::value ? G::TSPLIT : 0)> s3;
-            if constexpr (LateS2<P, T>::value) s3.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
+            constexpr bool LS2 = LateS2<P, T>::value && !SM::SHARED;
+            Stager<T, (LS2 ? G::TSPLIT : 0)> s3;
+            if constexpr (LS2) s3.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
+            // (SHARED: the image overwrites the layout-A tables -- every wave
+            // must be done with them first)
+            if constexpr (SM::SHARED) __syncthreads();
             exchange<T, NQR, false>(
                 L, H, c, lds,
                 [&]() {
-                    if constexpr (LateS2<P, T>::value) s3.commit((uint4*)(smem + SM::TAB1_OFF));
+                    if constexpr (LS2) s3.commit((uint4*)(smem + SM::TAB1_OFF));
                 },
                 [&]() {
                     if constexpr (SPLIT_FD) {
@@ -1404,12 +1430,15 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                     }
                 });
             RS16_STAMP(a, 4);
+            if constexpr (SM::SHARED) s3s.issue(a.skew_tab, TwiddleEntry<T>{a, c, 0, a.skew_fft});
             if constexpr (EARLY_B) {
                 Thr cs = c;
                 asm volatile("" : "+v"(cs.offL));
                 ifft_b_halves<T>(L, H, tab1, EvenStore<P, T>{a, cs});
             } else {
-                layers<P, T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1,
+                // (SHARED: the layout-B tables t >= TSPLIT sit beside the image)
+                const uint4* tab1b = SM::SHARED ? (const uint4*)(smem + SM::TABB_OFF) - G::TSPLIT * 5 : tab1;
+                layers<P, T, true, R, (T > 4 ? T : R), false, false, (ZERO_SKIP ? PR_ZERO : PR_NONE)>(L, H, c, a, tab1b,
                                                                                                     tab2, d.zmask);
             }
             in_b = true;
@@ -1465,6 +1494,11 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                 exchange<T, NQR, true>(L, H, c, lds, [&]() {
                     if constexpr (LateReveal<P, T>::value) rs.commit(a, c, smem);
                 });
+            }
+            if constexpr (SM::SHARED) {
+                // (the image is dead: every wave's rows are back in registers)
+                s3s.commit((uint4*)(smem + SM::TAB1_OFF));
+                __syncthreads();
             }
             RS16_STAMP(a, 8);
             prio<P, 4, T>();
