@@ -619,12 +619,31 @@ struct GroupLoop {
     }
 };
 
+// A uniform LDS address held in one VGPR.  Layout-B table addresses are
+// compile-time constants; left to the compiler, each ds_read gets its own
+// s_add + v_mov to build the address (150 VALU moves per ENC_MID item).
+// Through one opaque VGPR base the constant part folds into the ds_read
+// offset field instead.
+__device__ __forceinline__ const uint4* lds_vgpr(const uint4* p) {
+#ifndef RS16_NO_LDS_VBASE
+    uint32_t v = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4*)p;
+    asm volatile("" : "+v"(v));
+    return (const uint4*)(const __attribute__((address_space(3))) uint4*)(uintptr_t)v;
+#else
+    return p;
+#endif
+}
+
 // Apply the layers for k-bits [KB0, KB1) held in registers of layout LB.
 template <int P, int T, bool LB, int KB0, int KB1, bool FFT, bool IN_TAB2, int PRUNE = PR_NONE, class FIN = NoFin>
 __device__ __forceinline__ void layers(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const Thr& c,
                                        const PassArgs& a, const uint4* tab1, const uint4* tab2,
                                        uint32_t zmask = 0, const FIN& fin = FIN()) {
     if constexpr (KB1 > KB0) {
+        if constexpr (LB) {
+            if constexpr (IN_TAB2) tab2 = lds_vgpr(tab2);
+            else tab1 = lds_vgpr(tab1);
+        }
         uint32_t t0[20];
         load_table_lds(t0, group_table<T, LB, KB0, KB1, FFT, 0, IN_TAB2>(c, tab1, tab2));
         GroupLoop<P, T, LB, KB0, KB1, FFT, IN_TAB2, PRUNE, 0, FIN>::run(L, H, c, a, tab1, tab2, t0, zmask, fin);
@@ -1308,6 +1327,7 @@ template <int T, class FIN>
 __device__ __forceinline__ void ifft_b_halves(uint32_t (&L)[Geo<T>::NR], uint32_t (&H)[Geo<T>::NR], const uint4* tab1,
                                               const FIN& fin) {
     constexpr int e = HalfSeq<T>::at(0), kb = (e >> 4) & 15, gi = e & 15;
+    tab1 = lds_vgpr(tab1);
     uint32_t t0[20];
     load_table_lds(t0, tab1 + ((1 << T) - (1 << (T - kb)) + gi) * 5);
     HalfLoop<T, 0, FIN>::run(L, H, tab1, t0, fin);
