@@ -1231,12 +1231,16 @@ __device__ __forceinline__ void store_row(const PassArgs& a, const Thr& cs, uint
         const LaneOff<V32> lo(lr, a.S_rest, cs.offL);
         const int64_t shift = (int64_t)a.row_base_out - (a.rest_seg_b ? (int64_t)a.chunk : 0);
         const uint32_t k = kidx<T, END_B>(cs, m);
-        uint32_t tt[20];
-        load_table_lds(tt, rvt + k * 5);
-        uint32_t ol = 0, oh = 0;
-        mul_xor(ol, oh, L, H, tt);
-        st_ptr<NT>(a, lo.at(sgpr_ptr(a.rest + ((int64_t)ur + shift) * (int64_t)a.S_rest)), cs.active & (lostf[k] != 0),
-                   ol, oh);
+        // (a row that is not a lost original is neither multiplied nor
+        // stored: the branch is per row set, so a wave whose rows were all
+        // received skips the reveal -- most rows of a decode with few losses)
+        if (cs.active & (lostf[k] != 0)) {
+            uint32_t tt[20];
+            load_table_lds(tt, rvt + k * 5);
+            uint32_t ol = 0, oh = 0;
+            mul_xor(ol, oh, L, H, tt);
+            st_ptr<NT>(a, lo.at(sgpr_ptr(a.rest + ((int64_t)ur + shift) * (int64_t)a.S_rest)), true, ol, oh);
+        }
     }
 }
 template <int P, int T, bool V32>

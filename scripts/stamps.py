@@ -11,7 +11,8 @@ direction done, 6 formal derivative, 7 layout-B FFT layers, 8 layout
 switch, 9 last layers, 10 stores issued, 11 stores done; EVAL_POLY (the
 n <= 2048 eval kernel, rs16_misc.hip): 0 start, 1 flags in, 2 sums done,
 10 store issued, 11 store done.  Programs: RS16_STAMP_PROGS (comma list);
-size: argv[1] (k = m)."""
+size: argv[1] (k = m); loss pattern: RS16_STAMPS_LOSS, RS16_STAMPS_SCATTER
+(below)."""
 import ctypes as C
 import json
 import os
@@ -42,13 +43,20 @@ def main():
     # RS16_STAMPS_LOSS=L: the decode loses the last L originals and receives
     # recovery 0..L (the reference bench's 1 % pattern for L = k / 100);
     # default: every original lost (the half-transform decode)
+    # RS16_STAMPS_SCATTER=1: the L lost originals and the L received recovery
+    # shards are drawn at random instead (bench.py general_decodes)
     L = int(os.environ.get("RS16_STAMPS_LOSS", k))
     of = np.ones(k, np.uint8)
-    of[k - L:] = 0
     rf = np.zeros(m, np.uint8)
-    rf[:L] = 1
+    if os.environ.get("RS16_STAMPS_SCATTER"):
+        rng = np.random.default_rng(7)
+        of[rng.choice(k, L, replace=False)] = 0
+        rf[rng.choice(m, L, replace=False)] = 1
+    else:
+        of[k - L:] = 0
+        rf[:L] = 1
     held = original.copy()
-    held[k - L:] = 0
+    held[of == 0] = 0
     d_rest = DeviceArray.from_numpy(eng, held)
     d_of = DeviceArray.from_numpy(eng, of)
     d_rf = DeviceArray.from_numpy(eng, rf)
