@@ -1659,6 +1659,8 @@ __global__ void __launch_bounds__(Geo<T>::THREADS, ((P == DEC_SINGLE || P == DEC
         if (slot == 0) __builtin_amdgcn_s_setprio(3);
         else if (slot == 1) __builtin_amdgcn_s_setprio(2);
         else if (slot == 2) __builtin_amdgcn_s_setprio(1);
+        // (a second-slot sleep before the loads, 2 or 4 us, measured neutral
+        // to slower on the T = 7 passes: profiles/r06_t7_slot_sleep_rejected.txt)
     }
     TileStage<P, T> st;
     st.issue(a, c);  // twiddle tables first: they do not queue behind the tile
