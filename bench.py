@@ -832,15 +832,17 @@ def main():
 
     # The passes are bound by VALU issue, not HBM: the
     # same kernel against the VALU ceiling of this GF(2^16) butterfly.  A
-    # wave-quad-butterfly (4 elements per lane: 12 v_perm_b32, 10 selector
-    # ops, 6 v_bitop3_b32, 2 XORs = 30 VALU instructions) measured 115.7
-    # SIMD cycles at 8 waves per SIMD (119.9 at 4; tools/ubench_bfly.hip,
-    # profiles/r03_ubench_bfly.txt): v_perm_b32 issues every ~4.2 cycles at
-    # any occupancy and any stream that mixes it with single-rate ops runs at
-    # ~4 cycles per instruction (profiles/r03_ubench_mix.txt), although those
-    # ops alone issue every ~2.5 (profiles/r03_ubench_valu.txt).  Ceiling =
-    # 1024 SIMDs x 256 element-butterflies / 115.7 cycles at the 2.4 GHz peak
-    # clock.  Algorithmic work = element-butterflies of the pass's layers.
+    # wave-quad-butterfly (4 elements per lane: 12 v_perm_b32, 2 64-bit
+    # selector shifts, 6 masks, 6 v_bitop3_b32, 2 XORs = 28 VALU
+    # instructions) measured 110.4 SIMD cycles at 8 waves per SIMD (114.0 at
+    # 4; tools/ubench_bfly.hip, profiles/r06_ubench_bfly64.txt; 115.7 with
+    # the round-3 form's four 32-bit shifts): v_perm_b32 issues every ~4.2
+    # cycles at any occupancy and any stream that mixes it with single-rate
+    # ops runs at ~4 cycles per instruction (profiles/r03_ubench_mix.txt),
+    # although those ops alone issue every ~2.5 (profiles/r03_ubench_valu.txt).
+    # Ceiling = 1024 SIMDs x 256 element-butterflies / 110.4 cycles at the
+    # 2.4 GHz peak clock.  Algorithmic work = element-butterflies of the
+    # pass's layers.
     chunk = 1 << (m - 1).bit_length()
     L_e = chunk.bit_length() - 1
     lo_e, hi_e = L_e // 2, L_e - L_e // 2
@@ -849,12 +851,12 @@ def main():
     valu = None
     if layers is not None and L_e > 8:
         bfly = layers * (chunk // 2) * (S // 2)
-        peak = 1024 * 256 / 115.7 * 2.4e9
+        peak = 1024 * 256 / 110.4 * 2.4e9
         valu = {"bound": "valu", "kernel": dom, "achieved": round(bfly / dom_avg_s / 1e12, 3),
                 "peak": round(peak / 1e12, 3), "unit": "T element-butterflies/s", "frac": round(bfly / dom_avg_s / peak, 4),
                 "butterflies_per_launch": bfly,
-                "note": "measured issue ceiling of this kernel's butterfly (115.7 cycles per 30-instruction "
-                        "wave-quad-butterfly, profiles/r03_ubench_bfly.txt) at 2.4 GHz; the zero-twiddle groups "
+                "note": "measured issue ceiling of this kernel's butterfly (110.4 cycles per 28-instruction "
+                        "wave-quad-butterfly, profiles/r06_ubench_bfly64.txt) at 2.4 GHz; the zero-twiddle groups "
                         "the two-direction passes skip still count as butterflies here"}
 
     extra = {"serial_step" if args.split_decode else "split_decode_step": other_step}
