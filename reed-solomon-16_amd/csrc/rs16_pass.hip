@@ -269,7 +269,9 @@ __device__ __forceinline__ bool mid_need(const PassArgs& a, uint32_t& nlo, uint3
 // 2 first direction done, 3 layout-B FFT done, 4 last switch done, 5 stores).
 // (A static pair schedule -- slots 0-1 at priority 3 for the whole item,
 // slots 2-3 at 0 -- measured no better on the T = 7 passes and 3.5 us worse
-// on the T = 8 ones, same-box A/B x 3, round 4.)
+// on the T = 8 ones, same-box A/B x 3, round 4.  Round 6, two workgroups per
+// CU everywhere: without the schedule, or with a static bias for the younger
+// workgroup, ENC_MID runs 2-3 us slower: profiles/r06_prio_schedules_rejected.txt.)
 template <int P, int at, int T = 7> __device__ __forceinline__ void prio() {
     constexpr int v[6] = {3, 2, -1, 1, -1, 0};
     if constexpr (v[at] >= 0) __builtin_amdgcn_s_setprio(v[at]);
