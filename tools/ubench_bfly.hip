@@ -29,6 +29,36 @@ RS16_HD void mul_xor64(uint32_t& xL, uint32_t& xH, uint32_t yL, uint32_t yH, con
     xL = xor3(xor3(xL, l0, l1), xor3(l2, l3, l4), l5);
     xH = xor3(xor3(xH, h0, h1), xor3(h2, h3, h4), h5);
 }
+// the same multiply with its three instruction classes kept apart for the
+// scheduler (sched_barrier): selector ops, then the 12 perms, then the XOR
+// tree -- so that a wave issues long runs of one class
+RS16_HD void mul_xor64g(uint32_t& xL, uint32_t& xH, uint32_t yL, uint32_t yH, const uint32_t* t) {
+    const uint64_t y = ((uint64_t)yH << 32) | yL;
+    uint64_t a, b;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(a) : "v"(y));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(b) : "v"(y));
+#else
+    a = y >> 3, b = y >> 6;
+#endif
+    const uint32_t s0 = yL & 0x07070707u, s3 = yH & 0x07070707u;
+    const uint32_t s1 = (uint32_t)a & 0x07070707u, s4 = (uint32_t)(a >> 32) & 0x07070707u;
+    const uint32_t s2 = (uint32_t)b & 0x03030303u, s5 = (uint32_t)(b >> 32) & 0x03030303u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    const uint32_t l0 = perm(t[1], t[0], s0), h0 = perm(t[3], t[2], s0);
+    const uint32_t l1 = perm(t[5], t[4], s1), h1 = perm(t[7], t[6], s1);
+    const uint32_t l3 = perm(t[9], t[8], s3), h3 = perm(t[11], t[10], s3);
+    const uint32_t l4 = perm(t[13], t[12], s4), h4 = perm(t[15], t[14], s4);
+    const uint32_t l2 = perm(t[16], t[16], s2), h2 = perm(t[17], t[17], s2);
+    const uint32_t l5 = perm(t[18], t[18], s5), h5 = perm(t[19], t[19], s5);
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    xL = xor3(xor3(xL, l0, l1), xor3(l2, l3, l4), l5);
+    xH = xor3(xor3(xH, h0, h1), xor3(h2, h3, h4), h5);
+}
 #define ITER 256
 template <int MODE>
 __global__ void __launch_bounds__(256) k(unsigned* out, const unsigned* tab, unsigned long long* clk, unsigned seed) {
@@ -52,6 +82,9 @@ __global__ void __launch_bounds__(256) k(unsigned* out, const unsigned* tab, uns
                     L[m2] ^= L[m]; H[m2] ^= H[m];
                 } else if (MODE == 2) {  // FFT butterfly, 64-bit selector shifts
                     mul_xor64(L[m], H[m], L[m2], H[m2], t);
+                    L[m2] ^= L[m]; H[m2] ^= H[m];
+                } else if (MODE == 3) {  // the same, instruction classes grouped
+                    mul_xor64g(L[m], H[m], L[m2], H[m2], t);
                     L[m2] ^= L[m]; H[m2] ^= H[m];
                 } else {          // IFFT butterfly
                     L[m2] ^= L[m]; H[m2] ^= H[m];
@@ -100,12 +133,16 @@ int main() {
         const double g1 = g_ghz;
         float ms2 = run<2>(d, tab, blocks);
         const double g2 = g_ghz;
+        float ms3 = run<3>(d, tab, blocks);
+        const double g3 = g_ghz;
         (void)ms1;
         printf("waves/SIMD %d: FFT %.3f ms @ %.2f GHz (%.1f cyc/wave-bfly/SIMD = %.2f per instr of 30)  IFFT %.3f ms @ %.2f GHz (%.1f)\n",
                wps, ms0, g0, ms0 * 1e-3 * g0 * 1e9 * 1024 / bf, ms0 * 1e-3 * g0 * 1e9 * 1024 / bf / 30, ms1b, g1,
                ms1b * 1e-3 * g1 * 1e9 * 1024 / bf);
         printf("            FFT with 64-bit selector shifts %.3f ms @ %.2f GHz (%.1f cyc/wave-bfly/SIMD)\n", ms2, g2,
                ms2 * 1e-3 * g2 * 1e9 * 1024 / bf);
+        printf("            FFT, 64-bit shifts, classes grouped %.3f ms @ %.2f GHz (%.1f cyc/wave-bfly/SIMD)\n", ms3, g3,
+               ms3 * 1e-3 * g3 * 1e9 * 1024 / bf);
     }
     return 0;
 }

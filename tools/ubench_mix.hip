@@ -13,6 +13,7 @@
 //   P7 the multiply of rs16_gf.hpp (mul_xor) with the table in VGPRs (per-lane)
 //   P8 the same with the table wave-uniform (SGPR operands where the ISA allows)
 //   P9 perm + and (literal mask) alternating
+//   P10-P13 (round 6) grouped against interleaved perm / simple-op orders
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "../reed-solomon-16_amd/csrc/rs16_gf.hpp"
@@ -67,6 +68,22 @@ __global__ void __launch_bounds__(256) k(unsigned* out, const unsigned* tab, uns
                 if (i & 1) asm volatile("v_and_b32 %0, 0x7070707, %0" : "+v"(v[i]));
                 else asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(a[i]), "v"(b[i]));
             }
+            if (P == 10) {  // 8 perms, then 8 xors
+                if (i >= 8) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(v[i]) : "v"(a[i]));
+                else asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(a[i]), "v"(b[i]));
+            }
+            if (P == 11) {  // 4 perms, 4 xors, 4 perms, 4 xors
+                if (i & 4) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(v[i]) : "v"(a[i]));
+                else asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(a[i]), "v"(b[i]));
+            }
+            if (P == 12) {  // 12 perms, 4 bitop3 (the multiply's 12 : 6 mix, grouped)
+                if (i >= 12) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x96" : "+v"(v[i]) : "v"(a[i]), "v"(b[i]));
+                else asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(a[i]), "v"(b[i]));
+            }
+            if (P == 13) {  // the same 12 : 4 mix interleaved (3 perms, 1 bitop3)
+                if ((i & 3) == 3) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x96" : "+v"(v[i]) : "v"(a[i]), "v"(b[i]));
+                else asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(a[i]), "v"(b[i]));
+            }
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -118,6 +135,10 @@ int main() {
         run<5>(d, tab, dclk, cus, wps, "P5 perm+2xor", 16);
         run<6>(d, tab, dclk, cus, wps, "P6 perm+bitop3", 16);
         run<9>(d, tab, dclk, cus, wps, "P9 perm+and(lit)", 16);
+        run<10>(d, tab, dclk, cus, wps, "P10 8 perm, then 8 xor", 16);
+        run<11>(d, tab, dclk, cus, wps, "P11 4 perm, 4 xor (x2)", 16);
+        run<12>(d, tab, dclk, cus, wps, "P12 12 perm, then 4 bitop3", 16);
+        run<13>(d, tab, dclk, cus, wps, "P13 (3 perm, bitop3) x4", 16);
         run<7>(d, tab, dclk, cus, wps, "P7 mul_xor+xor (vgpr table)", 8 * 28 + 16);
         run<8>(d, tab, dclk, cus, wps, "P8 mul_xor+xor (uniform table)", 8 * 28 + 16);
     }
