@@ -1532,6 +1532,18 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
         }
         bool need = true;
         if constexpr (P == DEC_MID) need = (c.s << R) < a.need_hi && ((c.s + 1) << R) > a.need_lo;
+#ifndef RS16_NO_RESTORE_SKIP
+        if constexpr (PT::STORE == ST_RESTORE && T > 4) {
+            // a row set without a lost original stores nothing: its
+            // layout-A FFT layers are skipped (a wave whose two row sets
+            // both have none skips them -- most waves of a decode that lost
+            // few, scattered originals)
+            uint32_t any = 0;
+#pragma unroll
+            for (int m = 0; m < NR; m++) any |= lostf[kidx<T, false>(c, m)];
+            need = any != 0;
+        }
+#endif
         // second direction's layout-A tables: restaged into tab1 (T > 4), else in tab2
         if constexpr (EARLY) {
             Thr cs = c;
