@@ -146,6 +146,9 @@ template <int P, int T, int QL> struct SmemL;
 #ifndef RS16_MID_SHARED
 #define RS16_MID_SHARED 1
 #endif
+#ifndef RS16_DEC_MID_SHARED
+#define RS16_DEC_MID_SHARED 1
+#endif
 template <int P, int T> struct Rnd {
     static constexpr int NQR = T >= 7 && SmemL<P, T, Geo<T>::Q>::BYTES > RS16_ONE_ROUND_MAX ? 2 : 1;
     static constexpr int QL = Geo<T>::Q / NQR;
@@ -166,7 +169,7 @@ template <int P, int T, int QL> struct SmemL {
     // SHARED (ENC_MID at T = 8, one round): [image 64 KiB, holding the
     // layout-A tables of each direction outside the switches][IFFT layout-B
     // tables][FFT layout-B tables]
-    static constexpr bool SHARED = RS16_MID_SHARED && P == ENC_MID && T == 8 && QL == Geo<T>::Q;
+    static constexpr bool SHARED = RS16_MID_SHARED && (P == ENC_MID || (P == DEC_MID && RS16_DEC_MID_SHARED)) && T == 8 && QL == Geo<T>::Q;
     static constexpr int ERT_BYTES = PT::LOAD == LD_GATHER_DEC ? (1 << T) * 80 : 0;
     static constexpr int ERT_OFF = IMG_BYTES;
     static constexpr int TABB_OFF = IMG_BYTES;  // (SHARED: the IFFT's layout-B tables)
@@ -1522,7 +1525,12 @@ __device__ __forceinline__ void process_item(const PassArgs& a, const Thr& c, ui
                 });
             }
             if constexpr (SM::SHARED) {
-                // (the image is dead: every wave's rows are back in registers)
+                // (the image is dead once every wave's rows are back in
+                // registers: exchange() ends with a barrier, few_switch()
+                // does not)
+                if constexpr (SPLIT_FD) {
+                    if (fd_few) __syncthreads();
+                }
                 s3s.commit((uint4*)(smem + SM::TAB1_OFF));
                 __syncthreads();
             }
